@@ -1,0 +1,253 @@
+"""btsha1 -- ctypes binding of libbtsha1.so (the C-ABI in include/bt_sha1.h).
+
+This is the binding a Python caller (tests, bench.py) uses; C callers link the
+library directly.  Device buffers are passed as raw integer
+addresses (e.g. ``tensor.data_ptr()``) and streams as raw ``hipStream_t``
+handles (``torch.cuda.current_stream().cuda_stream``), so nothing here depends
+on torch.  There is no fallback: if the library cannot be loaded, importing
+this module raises, and every call that fails on the GPU raises BtSha1Error
+with the library's own message.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("BT_SHA1_LIB", os.path.join(HERE, "libbtsha1.so"))
+CHUNK = 512 * 1024  # BT_CHUNK_SIZE, chunk.h:16
+DIGEST = 20  # SHA1_HASH_SIZE, sha.h:34
+
+
+class BtSha1Error(RuntimeError):
+    pass
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libbtsha1.so not built at {LIB_PATH}: run `make` (or __graft_entry__.build())")
+lib = ctypes.CDLL(LIB_PATH)
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+_i64 = ctypes.c_int64
+
+
+class Verdict(ctypes.Structure):
+    _fields_ = [("tag", ctypes.c_uint64), ("ok", ctypes.c_int32), ("digest", ctypes.c_uint8 * 20)]
+
+
+class SHA1Context(ctypes.Structure):  # include/sha.h (reference sha.h:39-50 layout)
+    _fields_ = [("totalLength", ctypes.c_uint64), ("hash", ctypes.c_uint32 * 5),
+                ("bufferLength", ctypes.c_uint32), ("buffer", ctypes.c_uint8 * 64)]
+
+
+def _sig(name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_sig("bt_sha1_device_count", ctypes.c_int)
+_sig("bt_sha1_set_device", ctypes.c_int, ctypes.c_int)
+_sig("bt_sha1_last_error", ctypes.c_char_p)
+_sig("bt_sha1_build_info", ctypes.c_char_p)
+_sig("bt_sha1_set_ring_depth", ctypes.c_int, ctypes.c_int)
+_sig("bt_sha1_chunks_dev", ctypes.c_int, _vp, _u64, _u64, _u64, _vp, _vp)
+_sig("bt_sha1_verify_dev", ctypes.c_int, _vp, _u64, _u64, _u64, _vp, _vp, _vp, _vp)
+_sig("bt_sha1_ragged_dev", ctypes.c_int, _vp, _vp, _vp, _u64, _vp, _vp)
+_sig("bt_sha1_fill_synthetic", ctypes.c_int, _vp, _u64, _u64, _u64, _vp)
+_sig("bt_sha1_chunks_host", _i64, _vp, _u64, _u64, _vp)
+_sig("bt_sha1_chunks_host_multi", _i64, _vp, _u64, _u64, _vp, ctypes.c_int)
+_sig("bt_sha1_chunks_file", _i64, _vp, _u64, _vp, _u64)
+_sig("bt_sha1_verifier_create", _vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32)
+_sig("bt_sha1_verifier_destroy", None, _vp)
+_sig("bt_sha1_verifier_slot", _vp, _vp)
+_sig("bt_sha1_verifier_commit", ctypes.c_int, _vp, ctypes.c_uint32, _vp, _u64)
+_sig("bt_sha1_verifier_submit", ctypes.c_int, _vp, _vp, ctypes.c_uint32, _vp, _u64)
+_sig("bt_sha1_verifier_flush", ctypes.c_int, _vp)
+_sig("bt_sha1_verifier_poll", ctypes.c_int, _vp, ctypes.POINTER(Verdict), ctypes.c_int)
+_sig("bt_sha1_verifier_drain", ctypes.c_int, _vp, ctypes.POINTER(Verdict), ctypes.c_int)
+_sig("bt_sha1_verifier_pending", _i64, _vp)
+_sig("SHA1Init", None, ctypes.POINTER(SHA1Context))
+_sig("SHA1Update", None, ctypes.POINTER(SHA1Context), _vp, ctypes.c_uint32)
+_sig("SHA1Final", None, ctypes.POINTER(SHA1Context), _vp)
+_sig("shahash", None, _vp, ctypes.c_int, _vp)
+_sig("binary2hex", None, _vp, ctypes.c_int, ctypes.c_char_p)
+_sig("hex2binary", None, ctypes.c_char_p, ctypes.c_int, _vp)
+
+
+def _check(rc, what):
+    if rc is None or (isinstance(rc, int) and rc < 0):
+        raise BtSha1Error(f"{what}: {lib.bt_sha1_last_error().decode()}")
+    return rc
+
+
+def last_error():
+    return lib.bt_sha1_last_error().decode()
+
+
+def device_count():
+    return lib.bt_sha1_device_count()
+
+
+def set_ring_depth(nbuf):
+    _check(lib.bt_sha1_set_ring_depth(nbuf), "set_ring_depth")
+
+
+def build_info():
+    return lib.bt_sha1_build_info().decode()
+
+
+# ---- device-resident (addresses are ints) ------------------------------------
+def chunks_dev(d_in, n, chunk_len, pitch, d_digests, stream=None):
+    _check(lib.bt_sha1_chunks_dev(d_in, n, chunk_len, pitch, d_digests, stream), "bt_sha1_chunks_dev")
+
+
+def verify_dev(d_in, n, chunk_len, pitch, d_expected, d_ok, d_digests=None, stream=None):
+    _check(lib.bt_sha1_verify_dev(d_in, n, chunk_len, pitch, d_expected, d_ok, d_digests, stream),
+           "bt_sha1_verify_dev")
+
+
+def ragged_dev(d_base, d_offsets, d_lens, n, d_digests, stream=None):
+    _check(lib.bt_sha1_ragged_dev(d_base, d_offsets, d_lens, n, d_digests, stream), "bt_sha1_ragged_dev")
+
+
+def fill_synthetic(d_buf, nbytes, first_word, seed, stream=None):
+    _check(lib.bt_sha1_fill_synthetic(d_buf, nbytes, first_word, seed, stream), "bt_sha1_fill_synthetic")
+
+
+# ---- host ------------------------------------------------------------------------
+def _host_buf(data):
+    if isinstance(data, (bytes, bytearray)):
+        b = (ctypes.c_uint8 * max(len(data), 1)).from_buffer_copy(bytes(data) or b"\0")
+        return b, len(data)
+    mv = memoryview(data).cast("B")
+    arr = (ctypes.c_uint8 * max(mv.nbytes, 1)).from_buffer(mv) if not mv.readonly else \
+        (ctypes.c_uint8 * max(mv.nbytes, 1)).from_buffer_copy(mv.tobytes() or b"\0")
+    return arr, mv.nbytes
+
+
+def chunks_host(data, chunk_len=CHUNK, ndev=None):
+    """Digests of data cut into chunk_len pieces (short last piece): list of 20-byte values."""
+    buf, n = _host_buf(data)
+    nch = (n + chunk_len - 1) // chunk_len
+    out = (ctypes.c_uint8 * max(20 * nch, 1))()
+    if ndev is None:
+        got = _check(lib.bt_sha1_chunks_host(buf, n, chunk_len, out), "bt_sha1_chunks_host")
+    else:
+        got = _check(lib.bt_sha1_chunks_host_multi(buf, n, chunk_len, out, ndev), "bt_sha1_chunks_host_multi")
+    raw = bytes(out)
+    return [raw[20 * i:20 * i + 20] for i in range(got)]
+
+
+def shahash(data):
+    """chunk.h:28 through the GPU (aborts the process on a GPU error, like the C call)."""
+    buf, n = _host_buf(data)
+    out = (ctypes.c_uint8 * 20)()
+    lib.shahash(buf, n, out)
+    return bytes(out)
+
+
+class Sha1:
+    """SHA1Init/SHA1Update/SHA1Final (sha.h:58-60) on a caller-owned context."""
+
+    def __init__(self):
+        self.ctx = SHA1Context()
+        lib.SHA1Init(ctypes.byref(self.ctx))
+
+    def update(self, data):
+        buf, n = _host_buf(data)
+        lib.SHA1Update(ctypes.byref(self.ctx), buf, n)
+        return self
+
+    def final(self):
+        out = (ctypes.c_uint8 * 20)()
+        lib.SHA1Final(ctypes.byref(self.ctx), out)
+        return bytes(out)
+
+
+def binary2hex(b):
+    out = ctypes.create_string_buffer(2 * len(b) + 1)
+    lib.binary2hex((ctypes.c_uint8 * max(len(b), 1)).from_buffer_copy(bytes(b) or b"\0"), len(b), out)
+    return out.value.decode()
+
+
+def hex2binary(h):
+    hb = h.encode() if isinstance(h, str) else bytes(h)
+    out = (ctypes.c_uint8 * max(len(hb) // 2, 1))()
+    lib.hex2binary(ctypes.create_string_buffer(hb, len(hb) + 1), len(hb), out)
+    return bytes(out)[:len(hb) // 2]
+
+
+def make_chunks_file(path, chunk_len=CHUNK):
+    """bt_sha1_chunks_file over an open FILE* (libc fopen through ctypes)."""
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = _vp
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [_vp]
+    size = os.path.getsize(path)
+    nch = (size + chunk_len - 1) // chunk_len
+    out = (ctypes.c_uint8 * max(20 * nch, 1))()
+    fp = libc.fopen(path.encode(), b"rb")
+    if not fp:
+        raise OSError(f"cannot open {path}")
+    try:
+        got = _check(lib.bt_sha1_chunks_file(fp, chunk_len, out, nch), "bt_sha1_chunks_file")
+    finally:
+        libc.fclose(fp)
+    raw = bytes(out)
+    return [raw[20 * i:20 * i + 20] for i in range(got)]
+
+
+class Verifier:
+    """Batched asynchronous verify (bt_sha1_verifier_*)."""
+
+    def __init__(self, device=0, chunk_len=CHUNK, batch=64, nstreams=2):
+        self.h = lib.bt_sha1_verifier_create(device, chunk_len, batch, nstreams)
+        if not self.h:
+            raise BtSha1Error(f"bt_sha1_verifier_create: {last_error()}")
+        self.chunk_len = chunk_len
+
+    def submit(self, chunk, expected, tag):
+        buf, n = _host_buf(chunk)
+        e = (ctypes.c_uint8 * 20).from_buffer_copy(bytes(expected))
+        _check(lib.bt_sha1_verifier_submit(self.h, buf, n, e, tag), "bt_sha1_verifier_submit")
+
+    def slot_fill(self, chunk, expected, tag):
+        """Zero-copy form: write into the pinned slot, then commit."""
+        p = lib.bt_sha1_verifier_slot(self.h)
+        if not p:
+            raise BtSha1Error(f"bt_sha1_verifier_slot: {last_error()}")
+        ctypes.memmove(p, bytes(chunk), len(chunk))
+        e = (ctypes.c_uint8 * 20).from_buffer_copy(bytes(expected))
+        _check(lib.bt_sha1_verifier_commit(self.h, len(chunk), e, tag), "bt_sha1_verifier_commit")
+
+    def _collect(self, fn, max_n=4096):
+        out = (Verdict * max_n)()
+        got = _check(fn(self.h, out, max_n), "verifier")
+        return [(out[i].tag, bool(out[i].ok), bytes(out[i].digest)) for i in range(got)]
+
+    def poll(self):
+        return self._collect(lib.bt_sha1_verifier_poll)
+
+    def drain(self):
+        res = []
+        while True:
+            r = self._collect(lib.bt_sha1_verifier_drain)
+            if not r:
+                return res
+            res += r
+
+    def pending(self):
+        return lib.bt_sha1_verifier_pending(self.h)
+
+    def close(self):
+        if self.h:
+            lib.bt_sha1_verifier_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,850 @@
+// bt_sha1_api.cpp -- the C-ABI of libbtsha1.so: the reference's sha.h/chunk.h
+// surface re-implemented over the gfx950 kernels, plus batch / verify /
+// multi-GPU entry points (include/bt_sha1.h).
+//
+// Reference interfaces replaced (yunfanye/Bittorrent-with-Congestion-Control):
+//   SHA1Init/SHA1Update/SHA1Final  sha.c:149-163, 453-527, 529-558 (sha.h:58-60)
+//   shahash                        chunk.c:33-49  (chunk.h:28)
+//   make_chunks                    chunk.c:13-25  (chunk.h:25)
+//   binary2hex / hex2binary        chunk.c:55-83  (chunk.h:31,34)
+//   hash + memcmp of save_chunk    util.c:304-337 (batched: bt_sha1_verifier_*)
+//
+// Host-side work here is bookkeeping only (staging, padding-byte layout, hex
+// formatting); every compression runs in a HIP kernel.  No CPU hashing path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bt_sha1.h"
+#include "chunk.h"
+#include "sha1_launch.h"
+
+namespace {
+
+thread_local std::string t_err;
+thread_local int t_dev = 0;
+std::atomic<int> g_nbuf{3};
+
+void set_err(const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  t_err = buf;
+}
+
+#define BT_CK(expr)                                                                  \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess) {                                                          \
+      set_err("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return -1;                                                                     \
+    }                                                                                \
+  } while (0)
+
+[[noreturn]] void die(const char *where) {
+  fprintf(stderr, "libbtsha1: %s: %s\n", where, t_err.c_str());
+  fflush(stderr);
+  abort();
+}
+
+// Grow-only device / pinned scratch.
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t need) {
+    if (need <= cap) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t sz = std::max<size_t>(need, 4096);
+    BT_CK(hipMalloc(&p, sz));
+    cap = sz;
+    return 0;
+  }
+  template <class T>
+  T *as() const { return static_cast<T *>(p); }
+};
+struct PinBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t need) {
+    if (need <= cap) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t sz = std::max<size_t>(need, 4096);
+    BT_CK(hipHostMalloc(&p, sz, hipHostMallocDefault));
+    cap = sz;
+    return 0;
+  }
+  template <class T>
+  T *as() const { return static_cast<T *>(p); }
+};
+
+// One double-buffered staging lane of the host pipelines.
+struct Lane {
+  hipStream_t s = nullptr;
+  hipEvent_t ev = nullptr;
+  PinBuf h_in, h_dig;
+  DevBuf d_in, d_dig;
+  bool busy = false;
+  uint64_t first = 0, count = 0;  // chunk range in flight
+};
+
+struct DevCtx {
+  int dev = 0;
+  std::mutex mu;
+  hipStream_t s = nullptr;  // drop-in calls
+  Lane lane[2];
+  DevBuf d_msg, d_state;
+  PinBuf h_msg, h_state;
+};
+
+std::mutex g_ctx_mu;
+std::vector<std::unique_ptr<DevCtx>> g_ctx;
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+DevCtx *ctx_for(int dev) {
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  int n = device_count();
+  if (n <= 0) {
+    set_err("no HIP device visible (hipGetDeviceCount = 0)");
+    return nullptr;
+  }
+  if (dev < 0 || dev >= n) {
+    set_err("device %d out of range (%d visible)", dev, n);
+    return nullptr;
+  }
+  if ((int)g_ctx.size() < n) g_ctx.resize(n);
+  if (!g_ctx[dev]) {
+    auto c = std::make_unique<DevCtx>();
+    c->dev = dev;
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) {
+      set_err("cannot initialise HIP device %d", dev);
+      return nullptr;
+    }
+    for (auto &l : c->lane) {
+      if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&l.ev, hipEventDisableTiming) != hipSuccess) {
+        set_err("cannot create streams on device %d", dev);
+        return nullptr;
+      }
+    }
+    g_ctx[dev] = std::move(c);
+  }
+  return g_ctx[dev].get();
+}
+
+hipStream_t pick_stream(void *stream, DevCtx *c) { return stream ? (hipStream_t)stream : c->s; }
+
+bool fast_layout(const void *d_in, uint64_t chunk_len, uint64_t pitch, const void *d_dig) {
+  return ((uintptr_t)d_in & 15) == 0 && (pitch & 15) == 0 && ((uintptr_t)d_dig & 3) == 0 &&
+         chunk_len <= pitch && pitch <= (64ull << 20) && chunk_len < (1ull << 32);
+}
+
+// Launch the right kernel(s) for n equal chunks of len bytes at pitch.
+int launch_chunks(const void *d_in, uint64_t n, uint64_t len, uint64_t pitch, uint8_t *d_dig, hipStream_t s) {
+  if (n == 0) return 0;
+  if (fast_layout(d_in, len, pitch, d_dig)) {
+    BT_CK(btsha1_launch_fixed(d_in, n, (uint32_t)pitch, (uint32_t)len, d_dig, nullptr, nullptr, s, g_nbuf.load()));
+  } else {
+    if (len >= (1ull << 32)) {
+      set_err("chunk_len %llu exceeds 4 GiB", (unsigned long long)len);
+      return -1;
+    }
+    BT_CK(btsha1_launch_ragged(d_in, nullptr, nullptr, pitch, (uint32_t)len, n, d_dig, s));
+  }
+  return 0;
+}
+
+// A contiguous host image: full chunks through the hot kernel, a short last
+// chunk (make_chunks' final fread, chunk.c:20) through the ragged kernel.
+int launch_image(const uint8_t *d_img, uint64_t bytes, uint64_t chunk_len, uint8_t *d_dig, hipStream_t s) {
+  const uint64_t nfull = bytes / chunk_len, rem = bytes % chunk_len;
+  if (launch_chunks(d_img, nfull, chunk_len, chunk_len, d_dig, s)) return -1;
+  if (rem) BT_CK(btsha1_launch_ragged(d_img + nfull * chunk_len, nullptr, nullptr, 0, (uint32_t)rem, 1,
+                                      d_dig + 20 * nfull, s));
+  return 0;
+}
+
+uint64_t batch_chunks_for(uint64_t chunk_len) {
+  const uint64_t target = 256ull << 20;  // bytes per staging buffer
+  return std::max<uint64_t>(1, target / chunk_len);
+}
+
+// Generic double-buffered pipeline: fill(lane, first_chunk, max_bytes) puts
+// up to max_bytes of the image into lane.h_in and returns the byte count
+// (< max_bytes only at the end); sink(first_chunk, count, digests) receives
+// digests in chunk order.
+template <class Fill, class Sink>
+int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, Fill fill, Sink sink) {
+  if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
+    set_err("chunk_len must be in [1, 4 GiB)");
+    return -1;
+  }
+  const uint64_t per = batch_chunks_for(chunk_len);
+  const uint64_t bytes_per = per * chunk_len;
+  for (auto &l : c->lane) {
+    if (l.h_in.ensure(bytes_per) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per) ||
+        l.d_dig.ensure(20 * per))
+      return -1;
+    l.busy = false;
+  }
+  auto drain = [&](Lane &l) -> int {
+    if (!l.busy) return 0;
+    BT_CK(hipEventSynchronize(l.ev));
+    sink(l.first, l.count, l.h_dig.as<uint8_t>());
+    l.busy = false;
+    return 0;
+  };
+  uint64_t next = 0;
+  int k = 0;
+  for (;;) {
+    Lane &l = c->lane[k & 1];
+    if (drain(l)) return -1;
+    int64_t got = fill(l, next, bytes_per);
+    if (got < 0) return -1;
+    if (got == 0) break;
+    const uint64_t cnt = ((uint64_t)got + chunk_len - 1) / chunk_len;
+    BT_CK(hipMemcpyAsync(l.d_in.p, l.h_in.p, (size_t)got, hipMemcpyHostToDevice, l.s));
+    if (launch_image(l.d_in.as<uint8_t>(), (uint64_t)got, chunk_len, l.d_dig.as<uint8_t>(), l.s)) return -1;
+    BT_CK(hipMemcpyAsync(l.h_dig.p, l.d_dig.p, 20 * cnt, hipMemcpyDeviceToHost, l.s));
+    BT_CK(hipEventRecord(l.ev, l.s));
+    l.busy = true;
+    l.first = next;
+    l.count = cnt;
+    next += cnt;
+    ++k;
+    if ((uint64_t)got < bytes_per) break;
+  }
+  // Older lane first so digests arrive in order.
+  if (drain(c->lane[k & 1]) || drain(c->lane[(k + 1) & 1])) return -1;
+  return (int64_t)next;
+}
+
+int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t chunk_len, uint8_t *h_dig) {
+  DevCtx *c = ctx_for(dev);
+  if (!c) return -1;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(dev) != hipSuccess) {
+    set_err("hipSetDevice(%d) failed", dev);
+    return -1;
+  }
+  uint64_t off = 0;
+  auto fill = [&](Lane &l, uint64_t, uint64_t max) -> int64_t {
+    const uint64_t n = std::min<uint64_t>(max, total - off);
+    memcpy(l.h_in.p, h_in + off, n);
+    off += n;
+    return (int64_t)n;
+  };
+  auto sink = [&](uint64_t first, uint64_t count, const uint8_t *d) { memcpy(h_dig + 20 * first, d, 20 * count); };
+  return run_pipeline(c, chunk_len, fill, sink);
+}
+
+template <class Sink>
+int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
+  DevCtx *c = ctx_for(dev);
+  if (!c) return -1;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(dev) != hipSuccess) {
+    set_err("hipSetDevice(%d) failed", dev);
+    return -1;
+  }
+  auto fill = [&](Lane &l, uint64_t, uint64_t max) -> int64_t {
+    // fread straight into pinned memory; short only at EOF (chunk.c:20).
+    size_t got = 0;
+    while (got < max) {
+      size_t r = fread(l.h_in.as<uint8_t>() + got, 1, (size_t)(max - got), fp);
+      if (r == 0) break;
+      got += r;
+    }
+    if (ferror(fp)) {
+      set_err("fread failed");
+      return -1;
+    }
+    return (int64_t)got;
+  };
+  return run_pipeline(c, chunk_len, fill, sink);
+}
+
+// Single message on the GPU (shahash): stage, ragged kernel, 20 bytes back.
+int hash_one(DevCtx *c, const uint8_t *buf, uint32_t len, uint8_t out[20]) {
+  if (c->h_msg.ensure((size_t)len + 64) || c->d_msg.ensure((size_t)len + 64) || c->d_state.ensure(64) ||
+      c->h_state.ensure(64))
+    return -1;
+  if (len) memcpy(c->h_msg.p, buf, len);
+  if (len) BT_CK(hipMemcpyAsync(c->d_msg.p, c->h_msg.p, len, hipMemcpyHostToDevice, c->s));
+  BT_CK(btsha1_launch_ragged(c->d_msg.p, nullptr, nullptr, 0, len, 1, c->d_state.as<uint8_t>(), c->s));
+  BT_CK(hipMemcpyAsync(c->h_state.p, c->d_state.p, 20, hipMemcpyDeviceToHost, c->s));
+  BT_CK(hipStreamSynchronize(c->s));
+  memcpy(out, c->h_state.p, 20);
+  return 0;
+}
+
+// Advance sc->hash over nblocks whole blocks at host address `blocks`.
+int midstate(DevCtx *c, uint32_t h[5], const uint8_t *blocks, uint64_t nblocks) {
+  if (!nblocks) return 0;
+  const size_t bytes = (size_t)nblocks * 64;
+  if (c->h_msg.ensure(bytes) || c->d_msg.ensure(bytes) || c->d_state.ensure(64) || c->h_state.ensure(64)) return -1;
+  memcpy(c->h_msg.p, blocks, bytes);
+  memcpy(c->h_state.p, h, 20);
+  BT_CK(hipMemcpyAsync(c->d_msg.p, c->h_msg.p, bytes, hipMemcpyHostToDevice, c->s));
+  BT_CK(hipMemcpyAsync(c->d_state.p, c->h_state.p, 20, hipMemcpyHostToDevice, c->s));
+  BT_CK(btsha1_launch_midstate(c->d_state.as<uint32_t>(), c->d_msg.p, nblocks, c->s));
+  BT_CK(hipMemcpyAsync(c->h_state.p, c->d_state.p, 20, hipMemcpyDeviceToHost, c->s));
+  BT_CK(hipStreamSynchronize(c->s));
+  memcpy(h, c->h_state.p, 20);
+  return 0;
+}
+
+DevCtx *dropin_ctx(const char *who) {
+  DevCtx *c = ctx_for(t_dev);
+  if (!c) die(who);
+  if (hipSetDevice(t_dev) != hipSuccess) {
+    set_err("hipSetDevice(%d) failed", t_dev);
+    die(who);
+  }
+  return c;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int bt_sha1_device_count(void) { return device_count(); }
+
+int bt_sha1_set_device(int device) {
+  int n = device_count();
+  if (device < 0 || device >= n) {
+    set_err("device %d out of range (%d visible)", device, n);
+    return -1;
+  }
+  t_dev = device;
+  return 0;
+}
+
+const char *bt_sha1_last_error(void) { return t_err.c_str(); }
+
+const char *bt_sha1_build_info(void) {
+  static char info[128];
+  snprintf(info, sizeof info, "libbtsha1 gfx950 hip%d.%d ring=%d", HIP_VERSION_MAJOR, HIP_VERSION_MINOR,
+           g_nbuf.load());
+  return info;
+}
+
+int bt_sha1_set_ring_depth(int nbuf) {
+  if (nbuf < 2 || nbuf > 4) {
+    set_err("ring depth must be 2, 3 or 4");
+    return -1;
+  }
+  g_nbuf.store(nbuf);
+  return 0;
+}
+
+int bt_sha1_chunks_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_t pitch, uint8_t *d_digests,
+                       void *stream) {
+  if (n && (!d_in || !d_digests)) {
+    set_err("null pointer");
+    return -1;
+  }
+  if (n > 1 && pitch < chunk_len) {
+    set_err("pitch < chunk_len");
+    return -1;
+  }
+  if (n == 1 && pitch < chunk_len) pitch = (chunk_len + 15) & ~15ull;
+  int dev = 0;
+  BT_CK(hipGetDevice(&dev));
+  DevCtx *c = ctx_for(dev);
+  if (!c) return -1;
+  return launch_chunks(d_in, n, chunk_len, pitch, d_digests, pick_stream(stream, c));
+}
+
+int bt_sha1_verify_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_t pitch, const uint8_t *d_expected,
+                       uint8_t *d_ok, uint8_t *d_digests, void *stream) {
+  if (n == 0) return 0;
+  if (!d_in || !d_expected || !d_ok) {
+    set_err("null pointer");
+    return -1;
+  }
+  if (!fast_layout(d_in, chunk_len, pitch, d_digests)) {
+    set_err("verify needs a 16-byte aligned layout with pitch <= 64 MiB");
+    return -1;
+  }
+  int dev = 0;
+  BT_CK(hipGetDevice(&dev));
+  DevCtx *c = ctx_for(dev);
+  if (!c) return -1;
+  BT_CK(btsha1_launch_fixed(d_in, n, (uint32_t)pitch, (uint32_t)chunk_len, d_digests, d_expected, d_ok,
+                            pick_stream(stream, c), g_nbuf.load()));
+  return 0;
+}
+
+int bt_sha1_ragged_dev(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens, uint64_t n,
+                       uint8_t *d_digests, void *stream) {
+  if (n == 0) return 0;
+  if (!d_base || !d_offsets || !d_lens || !d_digests) {
+    set_err("null pointer");
+    return -1;
+  }
+  int dev = 0;
+  BT_CK(hipGetDevice(&dev));
+  DevCtx *c = ctx_for(dev);
+  if (!c) return -1;
+  BT_CK(btsha1_launch_ragged(d_base, d_offsets, d_lens, 0, 0, n, d_digests, pick_stream(stream, c)));
+  return 0;
+}
+
+int bt_sha1_fill_synthetic(void *d_buf, uint64_t nbytes, uint64_t first_word, uint64_t seed, void *stream) {
+  if (nbytes && (!d_buf || ((uintptr_t)d_buf & 15))) {
+    set_err("fill needs a non-null 16-byte aligned buffer");
+    return -1;
+  }
+  int dev = 0;
+  BT_CK(hipGetDevice(&dev));
+  DevCtx *c = ctx_for(dev);
+  if (!c) return -1;
+  BT_CK(btsha1_launch_fill(d_buf, nbytes, first_word, seed, pick_stream(stream, c)));
+  return 0;
+}
+
+int64_t bt_sha1_chunks_host(const void *h_in, uint64_t total_len, uint64_t chunk_len, uint8_t *h_digests) {
+  if (total_len && (!h_in || !h_digests)) {
+    set_err("null pointer");
+    return -1;
+  }
+  if (total_len == 0) return 0;
+  return chunks_host_on(t_dev, (const uint8_t *)h_in, total_len, chunk_len, h_digests);
+}
+
+int64_t bt_sha1_chunks_host_multi(const void *h_in, uint64_t total_len, uint64_t chunk_len, uint8_t *h_digests,
+                                  int ndev) {
+  if (chunk_len == 0) {
+    set_err("chunk_len must be > 0");
+    return -1;
+  }
+  if (total_len == 0) return 0;
+  const int avail = device_count();
+  if (avail <= 0) {
+    set_err("no HIP device visible");
+    return -1;
+  }
+  if (ndev <= 0 || ndev > avail) ndev = avail;
+  const uint64_t n = (total_len + chunk_len - 1) / chunk_len;
+  if ((uint64_t)ndev > n) ndev = (int)n;
+  // Contiguous block split of the chunk index: device g gets
+  // [g*n/G, (g+1)*n/G); only the globally last chunk can be short.
+  std::vector<int64_t> rc(ndev, 0);
+  std::vector<std::string> errs(ndev);
+  std::vector<std::thread> th;
+  for (int g = 0; g < ndev; ++g) {
+    th.emplace_back([&, g] {
+      const uint64_t lo = n * g / ndev, hi = n * (g + 1) / ndev;
+      const uint64_t off = lo * chunk_len;
+      const uint64_t bytes = std::min<uint64_t>(hi * chunk_len, total_len) - off;
+      rc[g] = chunks_host_on(g, (const uint8_t *)h_in + off, bytes, chunk_len, h_digests + 20 * lo);
+      errs[g] = t_err;
+    });
+  }
+  for (auto &t : th) t.join();
+  for (int g = 0; g < ndev; ++g)
+    if (rc[g] < 0) {
+      t_err = "device " + std::to_string(g) + ": " + errs[g];
+      return -1;
+    }
+  return (int64_t)n;
+}
+
+int64_t bt_sha1_chunks_file(void *fp, uint64_t chunk_len, uint8_t *h_digests, uint64_t max_chunks) {
+  if (!fp || !h_digests) {
+    set_err("null pointer");
+    return -1;
+  }
+  bool overflow = false;
+  int64_t n = chunks_file_on(t_dev, (FILE *)fp, chunk_len, [&](uint64_t first, uint64_t count, const uint8_t *d) {
+    for (uint64_t i = 0; i < count; ++i) {
+      if (first + i >= max_chunks) {
+        overflow = true;
+        return;
+      }
+      memcpy(h_digests + 20 * (first + i), d + 20 * i, 20);
+    }
+  });
+  if (n >= 0 && overflow) {
+    set_err("file has more than max_chunks chunks");
+    return -1;
+  }
+  return n;
+}
+
+// ---- drop-in: chunk.h --------------------------------------------------------
+
+// chunk.c:13-25.  Same contract: reads fp to EOF in BT_CHUNK_SIZE pieces,
+// digest i -> chunk_hashes[i] (caller-sized, as make_chunks.c:32-45 does).
+int make_chunks(FILE *fp, uint8_t **chunk_hashes) {
+  if (!fp || !chunk_hashes) {
+    set_err("null pointer");
+    return -1;
+  }
+  int64_t n = chunks_file_on(t_dev, fp, BT_CHUNK_SIZE, [&](uint64_t first, uint64_t count, const uint8_t *d) {
+    for (uint64_t i = 0; i < count; ++i) memcpy(chunk_hashes[first + i], d + 20 * i, 20);
+  });
+  if (n < 0) {
+    fprintf(stderr, "make_chunks: %s\n", t_err.c_str());
+    return -1;
+  }
+  return (int)n;
+}
+
+// chunk.c:33-49 (int length, like the reference).
+void shahash(uint8_t *str, int len, uint8_t *hash) {
+  if (len < 0) {
+    set_err("negative length %d", len);
+    die("shahash");
+  }
+  DevCtx *c = dropin_ctx("shahash");
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hash_one(c, str, (uint32_t)len, hash)) die("shahash");
+}
+
+// chunk.c:55-61: "%.2x" per byte, NUL-terminated.
+void binary2hex(uint8_t *buf, int len, char *hex) {
+  static const char dig[] = "0123456789abcdef";
+  for (int i = 0; i < len; ++i) {
+    hex[2 * i] = dig[buf[i] >> 4];
+    hex[2 * i + 1] = dig[buf[i] & 15];
+  }
+  hex[len < 0 ? 0 : 2 * len] = 0;
+}
+
+// chunk.c:66-83: toupper, '0'..'9' -> 0..9, otherwise ch - ('A' - 10); no
+// validation (kept bug-compatible: garbage in, garbage out).
+static inline uint8_t hexval(char ch) {
+  if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);
+  return (uint8_t)(ch <= '9' ? ch - '0' : ch - ('A' - 10));
+}
+void hex2binary(char *hex, int len, uint8_t *buf) {
+  for (int i = 0; i < len; i += 2) buf[i / 2] = (uint8_t)((hexval(hex[i]) << 4) | hexval(hex[i + 1]));
+}
+
+// ---- drop-in: sha.h ------------------------------------------------------------
+
+void SHA1Init(SHA1Context *sc) {  // sha.c:149-163
+  sc->totalLength = 0;
+  sc->hash[0] = 0x67452301u;
+  sc->hash[1] = 0xefcdab89u;
+  sc->hash[2] = 0x98badcfeu;
+  sc->hash[3] = 0x10325476u;
+  sc->hash[4] = 0xc3d2e1f0u;
+  sc->bufferLength = 0;
+}
+
+// sha.c:453-527: bytes top up the 64-byte staging block; every completed
+// block (the staged one plus all whole blocks of `data`) is compressed in one
+// GPU call; the remainder is staged.  totalLength counts bits like sha.c:511.
+void SHA1Update(SHA1Context *sc, const void *vdata, uint32_t len) {
+  if (!len) return;
+  const uint8_t *p = (const uint8_t *)vdata;
+  sc->totalLength += (uint64_t)len * 8u;
+  uint32_t take = 0;
+  if (sc->bufferLength) {
+    take = std::min<uint32_t>(64u - sc->bufferLength, len);
+    memcpy(sc->buffer.bytes + sc->bufferLength, p, take);
+    sc->bufferLength += take;
+    p += take;
+    len -= take;
+    if (sc->bufferLength < 64u) return;
+  }
+  const uint64_t nfull = len / 64u;
+  const bool staged_full = sc->bufferLength == 64u;
+  if (staged_full || nfull) {
+    DevCtx *c = dropin_ctx("SHA1Update");
+    std::lock_guard<std::mutex> g(c->mu);
+    std::vector<uint8_t> tmp;
+    const uint8_t *blocks = p;
+    uint64_t nb = nfull;
+    if (staged_full) {
+      tmp.resize(64 * (nfull + 1));
+      memcpy(tmp.data(), sc->buffer.bytes, 64);
+      if (nfull) memcpy(tmp.data() + 64, p, 64 * nfull);
+      blocks = tmp.data();
+      nb = nfull + 1;
+    }
+    if (midstate(c, sc->hash, blocks, nb)) die("SHA1Update");
+    sc->bufferLength = 0;
+  }
+  const uint32_t rest = len - (uint32_t)(64u * nfull);
+  if (rest) {
+    memcpy(sc->buffer.bytes, p + 64u * nfull, rest);
+    sc->bufferLength = rest;
+  }
+}
+
+// sha.c:529-558: 0x80, zeros to 56 mod 64, 64-bit big-endian bit count; the
+// last one or two blocks are compressed on the GPU; digest big-endian.
+void SHA1Final(SHA1Context *sc, uint8_t hash[SHA1_HASH_SIZE]) {
+  const uint32_t bl = sc->bufferLength;
+  uint32_t npad = 120u - bl;
+  if (npad > 64u) npad -= 64u;
+  uint8_t blk[128];
+  memset(blk, 0, sizeof blk);
+  memcpy(blk, sc->buffer.bytes, bl);
+  blk[bl] = 0x80;
+  const uint64_t bits = sc->totalLength;
+  const uint32_t end = bl + npad + 8u;  // 64 or 128
+  for (int i = 0; i < 8; ++i) blk[end - 8 + i] = (uint8_t)(bits >> (56 - 8 * i));
+  DevCtx *c = dropin_ctx("SHA1Final");
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (midstate(c, sc->hash, blk, end / 64u)) die("SHA1Final");
+  }
+  sc->totalLength += (uint64_t)(npad + 8u) * 8u;
+  sc->bufferLength = 0;
+  if (hash)
+    for (int i = 0; i < SHA1_HASH_WORDS; ++i) {
+      hash[4 * i] = (uint8_t)(sc->hash[i] >> 24);
+      hash[4 * i + 1] = (uint8_t)(sc->hash[i] >> 16);
+      hash[4 * i + 2] = (uint8_t)(sc->hash[i] >> 8);
+      hash[4 * i + 3] = (uint8_t)sc->hash[i];
+    }
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Batched asynchronous verifier (util.c:304-337 without the synchronous hash).
+// ===========================================================================
+struct VBatch {
+  hipStream_t s = nullptr;
+  hipEvent_t ev = nullptr;
+  uint8_t *h_in = nullptr, *h_exp = nullptr, *h_ok = nullptr, *h_dig = nullptr;
+  uint8_t *d_in = nullptr, *d_exp = nullptr, *d_ok = nullptr, *d_dig = nullptr;
+  std::vector<uint64_t> tags;
+  uint32_t count = 0;
+  bool inflight = false;
+};
+
+struct bt_sha1_verifier {
+  int dev = 0;
+  uint32_t chunk_len = 0, batch = 0;
+  std::vector<VBatch> b;
+  uint32_t fill = 0;             // batch being filled
+  std::deque<uint32_t> order;    // batches in flight, oldest first
+  std::deque<bt_sha1_verdict> done;
+  bool slot_out = false;
+  int64_t queued = 0;            // committed, verdict not yet returned
+};
+
+namespace {
+
+int v_harvest(bt_sha1_verifier *v, VBatch &b) {
+  BT_CK(hipEventSynchronize(b.ev));
+  for (uint32_t i = 0; i < b.count; ++i) {
+    bt_sha1_verdict r;
+    r.tag = b.tags[i];
+    r.ok = b.h_ok[i] ? 1 : 0;
+    memcpy(r.digest, b.h_dig + 20 * i, 20);
+    v->done.push_back(r);
+  }
+  b.count = 0;
+  b.inflight = false;
+  return 0;
+}
+
+int v_launch(bt_sha1_verifier *v) {
+  VBatch &b = v->b[v->fill];
+  if (b.count == 0) return 0;
+  const size_t bytes = (size_t)b.count * v->chunk_len;
+  BT_CK(hipMemcpyAsync(b.d_in, b.h_in, bytes, hipMemcpyHostToDevice, b.s));
+  BT_CK(hipMemcpyAsync(b.d_exp, b.h_exp, 20 * (size_t)b.count, hipMemcpyHostToDevice, b.s));
+  BT_CK(btsha1_launch_fixed(b.d_in, b.count, v->chunk_len, v->chunk_len, b.d_dig, b.d_exp, b.d_ok, b.s,
+                            g_nbuf.load()));
+  BT_CK(hipMemcpyAsync(b.h_ok, b.d_ok, b.count, hipMemcpyDeviceToHost, b.s));
+  BT_CK(hipMemcpyAsync(b.h_dig, b.d_dig, 20 * (size_t)b.count, hipMemcpyDeviceToHost, b.s));
+  BT_CK(hipEventRecord(b.ev, b.s));
+  b.inflight = true;
+  v->order.push_back(v->fill);
+  v->fill = (v->fill + 1) % (uint32_t)v->b.size();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32_t batch, uint32_t nstreams) {
+  if (chunk_len == 0 || (chunk_len & 15) || chunk_len > (64u << 20) || batch == 0) {
+    set_err("verifier: chunk_len must be a 16-byte multiple <= 64 MiB and batch > 0");
+    return nullptr;
+  }
+  if (!ctx_for(device)) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) {
+    set_err("hipSetDevice(%d) failed", device);
+    return nullptr;
+  }
+  auto *v = new bt_sha1_verifier;
+  v->dev = device;
+  v->chunk_len = chunk_len;
+  v->batch = batch;
+  v->b.resize(std::max<uint32_t>(nstreams, 2));
+  const size_t bytes = (size_t)batch * chunk_len;
+  for (auto &b : v->b) {
+    b.tags.resize(batch);
+    if (hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc((void **)&b.h_in, bytes, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&b.h_exp, 20 * (size_t)batch, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&b.h_ok, batch, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&b.h_dig, 20 * (size_t)batch, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc((void **)&b.d_in, bytes) != hipSuccess || hipMalloc((void **)&b.d_exp, 20 * (size_t)batch) != hipSuccess ||
+        hipMalloc((void **)&b.d_ok, batch) != hipSuccess || hipMalloc((void **)&b.d_dig, 20 * (size_t)batch) != hipSuccess) {
+      set_err("verifier: allocation failed");
+      bt_sha1_verifier_destroy(v);
+      return nullptr;
+    }
+  }
+  return v;
+}
+
+void bt_sha1_verifier_destroy(bt_sha1_verifier *v) {
+  if (!v) return;
+  (void)hipSetDevice(v->dev);
+  for (auto &b : v->b) {
+    if (b.s) (void)hipStreamSynchronize(b.s);
+    if (b.ev) (void)hipEventDestroy(b.ev);
+    if (b.s) (void)hipStreamDestroy(b.s);
+    if (b.h_in) (void)hipHostFree(b.h_in);
+    if (b.h_exp) (void)hipHostFree(b.h_exp);
+    if (b.h_ok) (void)hipHostFree(b.h_ok);
+    if (b.h_dig) (void)hipHostFree(b.h_dig);
+    if (b.d_in) (void)hipFree(b.d_in);
+    if (b.d_exp) (void)hipFree(b.d_exp);
+    if (b.d_ok) (void)hipFree(b.d_ok);
+    if (b.d_dig) (void)hipFree(b.d_dig);
+  }
+  delete v;
+}
+
+uint8_t *bt_sha1_verifier_slot(bt_sha1_verifier *v) {
+  if (!v) return nullptr;
+  if (hipSetDevice(v->dev) != hipSuccess) return nullptr;
+  VBatch &b = v->b[v->fill];
+  if (b.inflight) {  // ring wrapped: wait for this batch, keep its verdicts
+    while (!v->order.empty()) {
+      uint32_t o = v->order.front();
+      v->order.pop_front();
+      if (v_harvest(v, v->b[o])) return nullptr;
+      if (o == v->fill) break;
+    }
+  }
+  v->slot_out = true;
+  return b.h_in + (size_t)b.count * v->chunk_len;
+}
+
+int bt_sha1_verifier_commit(bt_sha1_verifier *v, uint32_t len, const uint8_t expected[20], uint64_t tag) {
+  if (!v || !v->slot_out || !expected) {
+    set_err("verifier_commit without a slot");
+    return -1;
+  }
+  if (len != v->chunk_len) {
+    set_err("verifier: chunk of %u bytes, verifier built for %u", len, v->chunk_len);
+    return -1;
+  }
+  if (hipSetDevice(v->dev) != hipSuccess) return -1;
+  VBatch &b = v->b[v->fill];
+  memcpy(b.h_exp + 20 * (size_t)b.count, expected, 20);
+  b.tags[b.count] = tag;
+  ++b.count;
+  ++v->queued;
+  v->slot_out = false;
+  if (b.count == v->batch) return v_launch(v);
+  return 0;
+}
+
+int bt_sha1_verifier_submit(bt_sha1_verifier *v, const void *h_chunk, uint32_t len, const uint8_t expected[20],
+                            uint64_t tag) {
+  if (!v || !h_chunk) {
+    set_err("null pointer");
+    return -1;
+  }
+  if (len != v->chunk_len) {
+    set_err("verifier: chunk of %u bytes, verifier built for %u", len, v->chunk_len);
+    return -1;
+  }
+  uint8_t *slot = bt_sha1_verifier_slot(v);
+  if (!slot) return -1;
+  memcpy(slot, h_chunk, len);
+  return bt_sha1_verifier_commit(v, len, expected, tag);
+}
+
+int bt_sha1_verifier_flush(bt_sha1_verifier *v) {
+  if (!v) return -1;
+  if (hipSetDevice(v->dev) != hipSuccess) return -1;
+  if (v->slot_out) {
+    set_err("verifier_flush with an uncommitted slot");
+    return -1;
+  }
+  return v_launch(v);
+}
+
+static int v_take(bt_sha1_verifier *v, bt_sha1_verdict *out, int max) {
+  int n = 0;
+  while (n < max && !v->done.empty()) {
+    out[n++] = v->done.front();
+    v->done.pop_front();
+  }
+  v->queued -= n;
+  return n;
+}
+
+int bt_sha1_verifier_poll(bt_sha1_verifier *v, bt_sha1_verdict *out, int max) {
+  if (!v) return -1;
+  if (hipSetDevice(v->dev) != hipSuccess) return -1;
+  while (!v->order.empty()) {
+    VBatch &b = v->b[v->order.front()];
+    hipError_t q = hipEventQuery(b.ev);
+    if (q == hipErrorNotReady) break;
+    if (q != hipSuccess) {
+      set_err("verifier: %s", hipGetErrorString(q));
+      return -1;
+    }
+    v->order.pop_front();
+    if (v_harvest(v, b)) return -1;
+  }
+  return v_take(v, out, max);
+}
+
+int bt_sha1_verifier_drain(bt_sha1_verifier *v, bt_sha1_verdict *out, int max) {
+  if (!v) return -1;
+  if (bt_sha1_verifier_flush(v)) return -1;
+  while (!v->order.empty()) {
+    uint32_t o = v->order.front();
+    v->order.pop_front();
+    if (v_harvest(v, v->b[o])) return -1;
+  }
+  return v_take(v, out, max);
+}
+
+int64_t bt_sha1_verifier_pending(bt_sha1_verifier *v) { return v ? v->queued : -1; }
+
+}  // extern "C"

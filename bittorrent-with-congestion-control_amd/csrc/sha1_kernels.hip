@@ -1,0 +1,294 @@
+// sha1_kernels.hip -- gfx950 kernels of the SHA-1 chunk path + their launchers.
+//
+// Kernels (all one message per lane; SHA-1 is a serial Merkle-Damgard chain,
+// so parallelism is across chunks only -- SURVEY.md §7 "Serial chain"):
+//   k_sha1_fixed    the hot path: n equal-length chunks at a fixed pitch in HBM
+//                   (make_chunks' 512 KiB chunks, chunk.c:20-21; received-chunk
+//                   verify, util.c:311-313, when VERIFY).  Each lane streams its
+//                   own chunk through a register ring of NBUF 128-byte lines,
+//                   issuing line i+NBUF-1 while compressing line i, so HBM
+//                   latency hides inside one wave (only 2 waves/SIMD exist at
+//                   131072 chunks).  Loads are raw buffer loads off a per-wave
+//                   descriptor: per-lane 32-bit voffset = lane * pitch, the
+//                   line offset rides in the scalar soffset -> zero VALU
+//                   address arithmetic in the loop.
+//   k_sha1_ragged   arbitrary (offset, length) messages: shahash (chunk.c:33),
+//                   the short last chunk of make_chunks (chunk.c:20 when
+//                   fread returns < 512 KiB), ragged batches.
+//   k_sha1_midstate chaining-state update over whole blocks: the GPU side of
+//                   the streaming SHA1Update/SHA1Final API (sha.c:453-558).
+//   k_fill_synthetic  frozen counter-based generator (bench/test data in HBM).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sha1_device.h"
+#include "sha1_launch.h"
+
+namespace btsha1 {
+
+constexpr int kBlock = 256;  // 4 waves; 2 blocks per CU at 131072 chunks
+
+// ---------------------------------------------------------------------------
+// Hot path.
+// ---------------------------------------------------------------------------
+template <int NBUF>
+__device__ __forceinline__ void load_line(u32x4 (&q)[8], __amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
+                                          uint32_t soff) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff + 16 * j, 0);
+}
+
+__device__ __forceinline__ void compress_line(State &st, const u32x4 (&q)[8]) {
+  uint32_t w[16];
+  block_from_le(w, q[0], q[1], q[2], q[3]);
+  compress(st, w);
+  block_from_le(w, q[4], q[5], q[6], q[7]);
+  compress(st, w);
+}
+
+template <int NBUF, bool VERIFY>
+__global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sha1_fixed(const uint8_t *__restrict__ base, uint64_t n_chunks,
+                                                          uint32_t pitch, uint32_t len,
+                                                          uint8_t *__restrict__ digests,
+                                                          const uint8_t *__restrict__ expected,
+                                                          uint8_t *__restrict__ ok) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t chunk0 = (uint64_t)blockIdx.x * kBlock + (uint64_t)wave * 64u;  // wave-uniform
+  if (chunk0 >= n_chunks) return;
+  const uint64_t left = n_chunks - chunk0;
+  const uint32_t nvalid = left < 64 ? (uint32_t)left : 64u;
+  // Lanes past the end re-hash the wave's last chunk (no divergence, no store).
+  const uint32_t mine = lane < nvalid ? lane : nvalid - 1u;
+  const uint32_t voff = mine * pitch;
+  const uint32_t nrec = (nvalid - 1u) * pitch + ((len + 3u) & ~3u);  // bytes this wave may read
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(base + chunk0 * (uint64_t)pitch), (short)0, (int)nrec, 0x00020000);
+
+  State st;
+  st.init();
+  const uint32_t nblocks = len >> 6;
+  const uint32_t nlines = nblocks >> 1;
+  const uint32_t nmain = (nlines / NBUF) * NBUF;  // lines covered by the pipelined loop
+
+  if (nmain) {
+    u32x4 ring[NBUF][8];
+#pragma unroll
+    for (int i = 0; i < NBUF - 1; ++i) load_line<NBUF>(ring[i], rsrc, voff, (uint32_t)i * 128u);
+    for (uint32_t line = 0; line < nmain; line += NBUF) {
+#pragma unroll
+      for (int s = 0; s < NBUF; ++s) {
+        // Prefetch may run NBUF-1 lines past the chunk: it reads the next
+        // chunk's bytes or, past nrec, range-checked zeros; never used.
+        load_line<NBUF>(ring[(s + NBUF - 1) % NBUF], rsrc, voff, (line + s + NBUF - 1) * 128u);
+        // Pin the prefetch here: left alone, the scheduler sinks it to the
+        // loop end to cut register pressure and the ring degenerates into a
+        // vmcnt(0) at the loop head.
+        __builtin_amdgcn_sched_barrier(0);
+        compress_line(st, ring[s]);
+      }
+    }
+  }
+  // Remaining whole blocks (at most 2*NBUF-1 of them), loaded directly.
+  for (uint32_t b = nmain * 2; b < nblocks; ++b) {
+    uint32_t w[16];
+    const uint32_t o = b * 64u;
+    block_from_le(w, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o, 0),
+                  __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o + 16, 0),
+                  __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o + 32, 0),
+                  __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o + 48, 0));
+    compress(st, w);
+  }
+  // Tail bytes + MD padding (sha.c:536-543); r is uniform across the batch.
+  const uint32_t r = len & 63u;
+  uint32_t tail[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t have = r > 4u * j ? r - 4u * j : 0u;
+    uint32_t v = 0;
+    if (have) v = keep_be_bytes(bswap(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, nblocks * 64u + 4u * j, 0)), have);
+    tail[j] = v;
+  }
+  finish(st, tail, r, len);
+
+  if (lane < nvalid) {
+    const uint64_t idx = chunk0 + lane;
+    const uint32_t d0 = bswap(st.h0), d1 = bswap(st.h1), d2 = bswap(st.h2), d3 = bswap(st.h3), d4 = bswap(st.h4);
+    if (digests) {
+      uint32_t *o = (uint32_t *)(digests + idx * 20u);  // sha.c:550-553 big-endian bytes
+      o[0] = d0; o[1] = d1; o[2] = d2; o[3] = d3; o[4] = d4;
+    }
+    if constexpr (VERIFY) {  // util.c:311-313: memcmp(hash, chunk->hash, 20) == 0
+      const uint8_t *x = expected + idx * 20u;
+      uint32_t e[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        e[k] = (uint32_t)x[4 * k] | ((uint32_t)x[4 * k + 1] << 8) | ((uint32_t)x[4 * k + 2] << 16) |
+               ((uint32_t)x[4 * k + 3] << 24);
+      ok[idx] = (uint8_t)((e[0] == d0) & (e[1] == d1) & (e[2] == d2) & (e[3] == d3) & (e[4] == d4));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generic paths (64-bit addressing, any alignment).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t load_be_word(const uint8_t *p, uint32_t align) {
+  if (align == 0) return bswap(*(const uint32_t *)p);
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+
+__device__ __forceinline__ void absorb_blocks(State &st, const uint8_t *p, uint64_t nblocks) {
+  const uint32_t align = (uint32_t)((uintptr_t)p & 15u);
+  if (align == 0) {
+    const u32x4 *q = (const u32x4 *)p;
+    for (uint64_t b = 0; b < nblocks; ++b, q += 4) {
+      uint32_t w[16];
+      block_from_le(w, q[0], q[1], q[2], q[3]);
+      compress(st, w);
+    }
+  } else {
+    const uint32_t a4 = (uint32_t)((uintptr_t)p & 3u);
+    for (uint64_t b = 0; b < nblocks; ++b, p += 64) {
+      uint32_t w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = load_be_word(p + 4 * j, a4);
+      compress(st, w);
+    }
+  }
+}
+
+__device__ __forceinline__ void absorb_tail_and_finish(State &st, const uint8_t *p, uint32_t r, uint64_t len) {
+  uint32_t tail[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if ((uint32_t)(4 * j + b) < r) v |= (uint32_t)p[4 * j + b] << (24 - 8 * b);
+    tail[j] = v;
+  }
+  finish(st, tail, r, len);
+}
+
+// Message i = base[offsets[i] .. + lens[i]); with offsets == NULL the batch is
+// strided instead: message i = base[i*pitch .. + fixed_len).
+__global__ __launch_bounds__(kBlock) void k_sha1_ragged(const uint8_t *__restrict__ base,
+                                                        const uint64_t *__restrict__ offsets,
+                                                        const uint32_t *__restrict__ lens, uint64_t pitch,
+                                                        uint32_t fixed_len, uint64_t n,
+                                                        uint8_t *__restrict__ digests) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *p = base + (offsets ? offsets[i] : i * pitch);
+  const uint32_t len = offsets ? lens[i] : fixed_len;
+  State st;
+  st.init();
+  const uint64_t nb = len >> 6;
+  absorb_blocks(st, p, nb);
+  absorb_tail_and_finish(st, p + nb * 64u, len & 63u, len);
+  uint8_t *o = digests + i * 20u;
+  const uint32_t h[5] = {st.h0, st.h1, st.h2, st.h3, st.h4};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {  // byte stores: digests need no alignment here
+    o[4 * k] = (uint8_t)(h[k] >> 24);
+    o[4 * k + 1] = (uint8_t)(h[k] >> 16);
+    o[4 * k + 2] = (uint8_t)(h[k] >> 8);
+    o[4 * k + 3] = (uint8_t)h[k];
+  }
+}
+
+// state[5] (host-order words, as SHA1Context.hash) advanced over nblocks blocks.
+__global__ void k_sha1_midstate(uint32_t *__restrict__ state, const uint8_t *__restrict__ p, uint64_t nblocks) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  State st{state[0], state[1], state[2], state[3], state[4]};
+  absorb_blocks(st, p, nblocks);
+  state[0] = st.h0; state[1] = st.h1; state[2] = st.h2; state[3] = st.h3; state[4] = st.h4;
+}
+
+// ---------------------------------------------------------------------------
+// Frozen synthetic generator: word g of the stream = splitmix64(seed + g),
+// stored little-endian (mirrored by oracle/sha1_oracle.c:or_fill_synthetic).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_synthetic(uint8_t *__restrict__ buf, uint64_t nbytes,
+                                                           uint64_t first_word, uint64_t seed) {
+  const uint64_t nw = nbytes >> 3;
+  const uint64_t npairs = nw >> 1;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const uint64_t s0 = seed + first_word;
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  for (uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x; p < npairs; p += stride) {
+    u64x2 v;
+    v.x = splitmix64(s0 + 2 * p);
+    v.y = splitmix64(s0 + 2 * p + 1);
+    *(u64x2 *)(buf + 16 * p) = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (uint64_t g = npairs * 2; g * 8 < nbytes; ++g) {
+      const uint64_t v = splitmix64(s0 + g);
+      for (uint64_t b = 0; b < 8 && g * 8 + b < nbytes; ++b) buf[g * 8 + b] = (uint8_t)(v >> (8 * b));
+    }
+  }
+}
+
+}  // namespace btsha1
+
+// ---------------------------------------------------------------------------
+// Launchers (C++ linkage, used by the C-ABI layer in bt_sha1_api.cpp).
+// ---------------------------------------------------------------------------
+using namespace btsha1;
+
+template <int NBUF>
+static hipError_t launch_fixed_nbuf(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
+                                    const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s) {
+  const uint64_t grid = (n + kBlock - 1) / kBlock;
+  if (d_ok)
+    hipLaunchKernelGGL((k_sha1_fixed<NBUF, true>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
+                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok);
+  else
+    hipLaunchKernelGGL((k_sha1_fixed<NBUF, false>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
+                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok);
+  return hipGetLastError();
+}
+
+hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
+                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int nbuf) {
+  if (n == 0) return hipSuccess;
+  switch (nbuf) {
+    case 2: return launch_fixed_nbuf<2>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
+    case 4: return launch_fixed_nbuf<4>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
+    default: return launch_fixed_nbuf<3>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
+  }
+}
+
+hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t pitch,
+                                uint32_t fixed_len, uint64_t n, uint8_t *d_dig, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t grid = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_sha1_ragged, dim3((uint32_t)grid), dim3(kBlock), 0, s, (const uint8_t *)d_base, d_off,
+                     d_len, pitch, fixed_len, n, d_dig);
+  return hipGetLastError();
+}
+
+hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_t nblocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_sha1_midstate, dim3(1), dim3(64), 0, s, d_state, (const uint8_t *)d_data, nblocks);
+  return hipGetLastError();
+}
+
+hipError_t btsha1_launch_fill(void *d_buf, uint64_t nbytes, uint64_t first_word, uint64_t seed, hipStream_t s) {
+  if (nbytes == 0) return hipSuccess;
+  uint64_t pairs = nbytes / 16;
+  uint64_t grid = (pairs + kBlock - 1) / kBlock;
+  if (grid > 8192) grid = 8192;
+  if (grid == 0) grid = 1;
+  hipLaunchKernelGGL(k_fill_synthetic, dim3((uint32_t)grid), dim3(kBlock), 0, s, (uint8_t *)d_buf, nbytes,
+                     first_word, seed);
+  return hipGetLastError();
+}

@@ -1,0 +1,19 @@
+// sha1_launch.h -- internal launcher interface between the kernels
+// (sha1_kernels.hip) and the C-ABI runtime (bt_sha1_api.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// n equal chunks of `len` bytes at `pitch` (16-byte multiple, 64*pitch < 4 GiB),
+// d_in 16-byte aligned.  d_dig: 20*n bytes (4-byte aligned) or NULL.  When
+// d_ok != NULL also compares against d_exp (20*n) and writes one byte per chunk.
+hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
+                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int nbuf);
+// n messages at d_base + d_off[i], d_len[i] bytes each; with d_off == NULL,
+// message i is at d_base + i*pitch, fixed_len bytes.  Any alignment.
+hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t pitch,
+                                uint32_t fixed_len, uint64_t n, uint8_t *d_dig, hipStream_t s);
+// d_state[5] advanced over nblocks whole 64-byte blocks at d_data.
+hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_t nblocks, hipStream_t s);
+// Synthetic stream words [first_word, first_word + nbytes/8) into d_buf (16-byte aligned).
+hipError_t btsha1_launch_fill(void *d_buf, uint64_t nbytes, uint64_t first_word, uint64_t seed, hipStream_t s);

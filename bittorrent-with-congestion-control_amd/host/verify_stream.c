@@ -1,0 +1,140 @@
+/*
+ * verify-stream -- the received-chunk verify path of the peer (util.c:250-337)
+ * driven through the batched GPU verifier, end to end from host memory.
+ *
+ *   verify-stream [-b batch] [-s streams] [-r rounds] [-x] <data-file> <chunks-file>
+ *
+ * For every chunk listed in <chunks-file> ("<id> <hex>" lines, as
+ * parse_has_get_chunk_file reads them, util.c:90-93) the chunk's bytes are
+ * "received" the way save_data_packet assembles them -- 1484-byte DATA
+ * payloads memcpy'd into the chunk buffer (util.c:275, common.h:30-31) -- but
+ * straight into a pinned verifier slot, then committed with the expected hash
+ * (util.c:311-313 becomes a batched GPU verify).  Verdicts are polled from the
+ * loop like a select() tick would.  A failed chunk prints "Verification
+ * failed!" exactly as util.c:317-318 does.  -x flips one byte of every 7th
+ * chunk to exercise the failure branch.  The last line is a JSON summary with
+ * the host->verdict rate.
+ */
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "bt_sha1.h"
+#include "chunk.h"
+
+#define PAYLOAD 1484 /* MAX_PAYLOAD_SIZE, common.h:30 */
+
+static double now(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+int main(int argc, char **argv) {
+  int batch = 64, streams = 2, rounds = 1, corrupt = 0, opt;
+  while ((opt = getopt(argc, argv, "b:s:r:x")) != -1) {
+    if (opt == 'b') batch = atoi(optarg);
+    else if (opt == 's') streams = atoi(optarg);
+    else if (opt == 'r') rounds = atoi(optarg);
+    else if (opt == 'x') corrupt = 1;
+    else {
+      fprintf(stderr, "usage: %s [-b batch] [-s streams] [-r rounds] [-x] <data-file> <chunks-file>\n", argv[0]);
+      return 255;
+    }
+  }
+  if (argc - optind != 2) {
+    fprintf(stderr, "usage: %s [-b batch] [-s streams] [-r rounds] [-x] <data-file> <chunks-file>\n", argv[0]);
+    return 255;
+  }
+  int fd = open(argv[optind], O_RDONLY);
+  struct stat st;
+  if (fd < 0 || fstat(fd, &st) != 0) {
+    perror(argv[optind]);
+    return 255;
+  }
+  const uint8_t *img = st.st_size ? (const uint8_t *)mmap(NULL, st.st_size, PROT_READ, MAP_PRIVATE, fd, 0) : NULL;
+  FILE *cf = fopen(argv[optind + 1], "r");
+  if (!cf) {
+    perror(argv[optind + 1]);
+    return 255;
+  }
+  int cap = 1024, n = 0;
+  int *ids = malloc(sizeof(int) * cap);
+  uint8_t *exp = malloc(20 * cap);
+  char line[256], hex[128];
+  while (fgets(line, sizeof line, cf)) {
+    int id;
+    if (line[0] == '#' || sscanf(line, "%d %127s", &id, hex) != 2 || strlen(hex) != 40) continue;
+    if (n == cap) {
+      cap *= 2;
+      ids = realloc(ids, sizeof(int) * cap);
+      exp = realloc(exp, 20 * cap);
+    }
+    ids[n] = id;
+    hex2binary(hex, 40, exp + 20 * n);
+    n++;
+  }
+  fclose(cf);
+
+  bt_sha1_verifier *v = bt_sha1_verifier_create(0, BT_CHUNK_SIZE, (uint32_t)batch, (uint32_t)streams);
+  if (!v) {
+    fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
+    return 255;
+  }
+  bt_sha1_verdict out[256];
+  long good = 0, bad = 0, total = 0;
+  double t0 = now();
+  for (int r = 0; r < rounds; r++) {
+    for (int k = 0; k < n; k++) {
+      const uint64_t off = (uint64_t)ids[k] * BT_CHUNK_SIZE;
+      if (off + BT_CHUNK_SIZE > (uint64_t)st.st_size) continue; /* only whole chunks are verified (util.c:307) */
+      uint8_t *slot = bt_sha1_verifier_slot(v);
+      if (!slot) {
+        fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
+        return 255;
+      }
+      for (uint32_t got = 0; got < BT_CHUNK_SIZE; got += PAYLOAD) { /* save_data_packet, util.c:275 */
+        uint32_t len = BT_CHUNK_SIZE - got < PAYLOAD ? BT_CHUNK_SIZE - got : PAYLOAD;
+        memcpy(slot + got, img + off + got, len);
+      }
+      if (corrupt && k % 7 == 3) slot[k % BT_CHUNK_SIZE] ^= 0x5a;
+      if (bt_sha1_verifier_commit(v, BT_CHUNK_SIZE, exp + 20 * k, (uint64_t)k)) {
+        fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
+        return 255;
+      }
+      total++;
+      int m;
+      while ((m = bt_sha1_verifier_poll(v, out, 256)) > 0)
+        for (int i = 0; i < m; i++) {
+          if (out[i].ok) good++;
+          else {
+            char h[41];
+            binary2hex(out[i].digest, 20, h);
+            printf("Hash: %s\nVerification failed!\n", h); /* util.c:316-318 */
+            bad++;
+          }
+        }
+    }
+  }
+  int m;
+  while ((m = bt_sha1_verifier_drain(v, out, 256)) > 0)
+    for (int i = 0; i < m; i++) {
+      if (out[i].ok) good++;
+      else {
+        char h[41];
+        binary2hex(out[i].digest, 20, h);
+        printf("Hash: %s\nVerification failed!\n", h);
+        bad++;
+      }
+    }
+  double dt = now() - t0;
+  bt_sha1_verifier_destroy(v);
+  printf("{\"chunks\": %ld, \"ok\": %ld, \"failed\": %ld, \"seconds\": %.6f, \"GiB_per_s\": %.4f, \"batch\": %d, \"streams\": %d}\n",
+         total, good, bad, dt, total * (double)BT_CHUNK_SIZE / dt / (1u << 30), batch, streams);
+  return bad && !corrupt ? 1 : 0;
+}

@@ -1,0 +1,120 @@
+/*
+ * bt_sha1.h -- C-ABI of the MI355X SHA-1 chunk-hashing path (libbtsha1.so).
+ *
+ * Drop-in surface (declared in sha.h / chunk.h of this directory, which keep
+ * the reference's prototypes source-compatible):
+ *   SHA1Init / SHA1Update / SHA1Final   replace reference sha.h:58-60
+ *   make_chunks / shahash               replace reference chunk.h:25,28
+ *   binary2hex / hex2binary             replace reference chunk.h:31,34
+ * Every digest is computed by the HIP kernels of
+ * bittorrent-with-congestion-control_amd/csrc/ on the GPU; there is no CPU
+ * hashing path in this library.  If no GPU / HIP runtime is usable the
+ * int-returning entry points return -1 (bt_sha1_last_error() says why) and
+ * the void ones (shahash, SHA1Update, SHA1Final) print the error and abort().
+ *
+ * Additions with no reference counterpart (batching is what makes a GPU pay):
+ * device-resident batches, ragged batches, a batched asynchronous verifier
+ * that replaces the synchronous shahash + memcmp of util.c:311-313, a host
+ * pipeline over pinned buffers, a multi-GPU host split, and the frozen
+ * synthetic generator used by the bench and the tests.
+ *
+ * Conventions: plain pointers and sizes; `stream` is a hipStream_t passed as
+ * void* (NULL = the library's own stream for the current device); device
+ * pointers are prefixed d_, host pointers h_.  Return 0 (or a count) on
+ * success, -1 on error.
+ */
+#ifndef BT_SHA1_H
+#define BT_SHA1_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "sha.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BT_SHA1_DIGEST_SIZE 20
+
+/* ---- runtime ---------------------------------------------------------- */
+/* Number of visible GPUs (0 if none), without creating any context. */
+int bt_sha1_device_count(void);
+/* Select the device used by the drop-in calls on this thread (default 0). */
+int bt_sha1_set_device(int device);
+/* Human-readable description of the last error on this thread. */
+const char *bt_sha1_last_error(void);
+/* Library / kernel build description (arch, ring depth). */
+const char *bt_sha1_build_info(void);
+/* Hot-kernel register-ring depth in 128-byte lines (2, 3 or 4; default 3). */
+int bt_sha1_set_ring_depth(int nbuf);
+
+/* ---- device-resident batches (the hot path) ---------------------------- */
+/* n chunks of chunk_len bytes, chunk i at d_in + i*pitch (pitch >= chunk_len).
+ * d_digests receives 20*n bytes, digest i = SHA-1(chunk i) as sha.c:545-556
+ * serialises it.  Fast path when d_in and pitch are 16-byte aligned and
+ * 64*pitch < 4 GiB; any other layout takes the generic kernel. */
+int bt_sha1_chunks_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_t pitch,
+                       uint8_t *d_digests, void *stream);
+/* Same, then compares with d_expected (20*n): d_ok[i] = 1 iff equal
+ * (util.c:311-313).  d_digests may be NULL. */
+int bt_sha1_verify_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_t pitch,
+                       const uint8_t *d_expected, uint8_t *d_ok, uint8_t *d_digests, void *stream);
+/* n messages, message i = d_base[d_offsets[i] .. + d_lens[i]). */
+int bt_sha1_ragged_dev(const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+                       uint64_t n, uint8_t *d_digests, void *stream);
+/* Frozen generator: 64-bit word g of the stream = splitmix64(seed + g), LE.
+ * Writes words first_word .. into d_buf (16-byte aligned), nbytes bytes. */
+int bt_sha1_fill_synthetic(void *d_buf, uint64_t nbytes, uint64_t first_word, uint64_t seed,
+                           void *stream);
+
+/* ---- host batches (H2D -> kernel -> D2H, double-buffered pinned staging) - */
+/* make_chunks over a memory image: chunk i = h_in[i*chunk_len ..], the last
+ * one may be short.  Returns the chunk count (ceil(total_len/chunk_len)). */
+int64_t bt_sha1_chunks_host(const void *h_in, uint64_t total_len, uint64_t chunk_len,
+                            uint8_t *h_digests);
+/* The same split over the first `ndev` GPUs (<=0: all), one host thread per
+ * device, contiguous chunk ranges, digests gathered into h_digests in order. */
+int64_t bt_sha1_chunks_host_multi(const void *h_in, uint64_t total_len, uint64_t chunk_len,
+                                  uint8_t *h_digests, int ndev);
+/* make_chunks over a FILE* with an explicit chunk size (make_chunks uses
+ * BT_CHUNK_SIZE).  h_digests must hold 20*ceil(size/chunk_len) bytes. */
+int64_t bt_sha1_chunks_file(void *fp /* FILE* */, uint64_t chunk_len, uint8_t *h_digests,
+                            uint64_t max_chunks);
+
+/* ---- batched asynchronous verify (replaces util.c:304-337's hash+memcmp) -- */
+typedef struct bt_sha1_verifier bt_sha1_verifier;
+typedef struct {
+  uint64_t tag;                       /* caller's tag (e.g. chunk id)        */
+  int32_t ok;                         /* 1: digest == expected, 0: mismatch  */
+  uint8_t digest[BT_SHA1_DIGEST_SIZE]; /* computed digest                    */
+} bt_sha1_verdict;
+
+/* batch: chunks per GPU launch; nstreams: batches in flight (>=2 overlaps
+ * H2D of batch k+1 with hashing of batch k); chunk_len: BT_CHUNK_SIZE. */
+bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32_t batch,
+                                          uint32_t nstreams);
+void bt_sha1_verifier_destroy(bt_sha1_verifier *v);
+/* Zero-copy: a pinned chunk_len-byte slot the caller assembles a chunk in
+ * (e.g. save_data_packet's memcpy target, util.c:275).  Blocks only if every
+ * slot is in flight.  NULL on error. */
+uint8_t *bt_sha1_verifier_slot(bt_sha1_verifier *v);
+/* Queue the slot last returned by bt_sha1_verifier_slot (len bytes used). */
+int bt_sha1_verifier_commit(bt_sha1_verifier *v, uint32_t len, const uint8_t expected[20], uint64_t tag);
+/* Copying form: slot + memcpy + commit. */
+int bt_sha1_verifier_submit(bt_sha1_verifier *v, const void *h_chunk, uint32_t len,
+                            const uint8_t expected[20], uint64_t tag);
+/* Launch the partially filled batch now. */
+int bt_sha1_verifier_flush(bt_sha1_verifier *v);
+/* Non-blocking: copy up to max finished verdicts out; returns the count. */
+int bt_sha1_verifier_poll(bt_sha1_verifier *v, bt_sha1_verdict *out, int max);
+/* Blocking: flush, wait for everything in flight, return up to max verdicts. */
+int bt_sha1_verifier_drain(bt_sha1_verifier *v, bt_sha1_verdict *out, int max);
+/* Verdicts not yet returned (in flight + finished-unpolled). */
+int64_t bt_sha1_verifier_pending(bt_sha1_verifier *v);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BT_SHA1_H */

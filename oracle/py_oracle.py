@@ -1,0 +1,122 @@
+"""oracle/py_oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes access to the CPU checkers:
+  * liboracle_sha1.so   our restatement of the reference (oracle/sha1_oracle.c)
+  * _ref/libref_sha1.so the reference's own chunk.c + sha.c, compiled from
+                        /root/reference by oracle/Makefile (present only where it
+                        was built; travels to the GPU box as a prebuilt file)
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module; the product (libbtsha1.so) never does.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle_sha1.so")
+REF_SO = os.path.join(HERE, "_ref", "libref_sha1.so")
+REF_SO_O0 = os.path.join(HERE, "_ref", "libref_sha1_O0.so")
+
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+
+_lib = ctypes.CDLL(ORACLE_SO)
+_lib.or_shahash.argtypes = [_vp, ctypes.c_int, _vp]
+_lib.or_fill_synthetic.argtypes = [_vp, _u64, _u64, _u64]
+_lib.or_hash_chunks.argtypes = [_vp, _u64, _u64, ctypes.c_uint32, ctypes.c_uint32, _vp, ctypes.c_int]
+_lib.or_hash_chunks.restype = ctypes.c_int
+_lib.or_sha1_init.argtypes = [_vp]
+_lib.or_sha1_update.argtypes = [_vp, _vp, ctypes.c_uint32]
+_lib.or_sha1_final.argtypes = [_vp, _vp]
+_lib.or_sha1_blocks.argtypes = [_vp, _vp, _u64]
+_lib.or_binary2hex.argtypes = [_vp, ctypes.c_int, ctypes.c_char_p]
+_lib.or_hex2binary.argtypes = [ctypes.c_char_p, ctypes.c_int, _vp]
+
+SEED_SYNTH = 0x0B175EED
+SEED_EDGE = 0x5EED0001
+SEED_TAIL = 0x7A11
+SEED_RAGGED = 0xABCD
+CHUNK = 512 * 1024
+
+
+def ragged_len(k):
+    """Length of message k of the committed ragged golden batch (tests/golden/make_golden.py)."""
+    return (k * 7919) % 2113 + (k % 5) * 64
+
+
+def _buf(data):
+    return (ctypes.c_uint8 * max(len(data), 1)).from_buffer_copy(bytes(data) or b"\0")
+
+
+def sha1(data) -> bytes:
+    out = (ctypes.c_uint8 * 20)()
+    _lib.or_shahash(_buf(data), len(data), out)
+    return bytes(out)
+
+
+class Sha1Stream:
+    def __init__(self):
+        self.ctx = ctypes.create_string_buffer(128)
+        _lib.or_sha1_init(self.ctx)
+
+    def update(self, data):
+        _lib.or_sha1_update(self.ctx, _buf(data), len(data))
+        return self
+
+    def final(self):
+        out = (ctypes.c_uint8 * 20)()
+        _lib.or_sha1_final(self.ctx, out)
+        return bytes(out)
+
+
+def fill_synthetic(nbytes, first_word, seed) -> bytearray:
+    buf = bytearray(max(nbytes, 1))
+    arr = (ctypes.c_uint8 * len(buf)).from_buffer(buf)
+    _lib.or_fill_synthetic(arr, nbytes, first_word, seed)
+    return buf[:nbytes] if nbytes else bytearray()
+
+
+def hash_chunks(data, chunk_len, pitch=None, nthreads=1, lib=None):
+    """Digests of equal chunks (short last one) in a host buffer, pthread-split."""
+    n_bytes = len(data)
+    pitch = pitch or chunk_len
+    n = (n_bytes + pitch - 1) // pitch if n_bytes else 0
+    last = n_bytes - (n - 1) * pitch if n else 0
+    last = min(last, chunk_len)
+    out = (ctypes.c_uint8 * max(20 * n, 1))()
+    if isinstance(data, bytearray):
+        src = (ctypes.c_uint8 * len(data)).from_buffer(data)
+    else:
+        src = _buf(data)
+    _lib.or_hash_chunks(src, n, pitch, chunk_len, last, out, nthreads)
+    raw = bytes(out)
+    return [raw[20 * i:20 * i + 20] for i in range(n)]
+
+
+def binary2hex(b) -> str:
+    out = ctypes.create_string_buffer(2 * len(b) + 1)
+    _lib.or_binary2hex(_buf(b), len(b), out)
+    return out.value.decode()
+
+
+def hex2binary(h) -> bytes:
+    hb = h.encode() if isinstance(h, str) else bytes(h)
+    out = (ctypes.c_uint8 * max(len(hb) // 2, 1))()
+    _lib.or_hex2binary(ctypes.create_string_buffer(hb, len(hb) + 1), len(hb), out)
+    return bytes(out)[:len(hb) // 2]
+
+
+def compress_blocks(state, blocks: bytes):
+    st = (ctypes.c_uint32 * 5)(*state)
+    _lib.or_sha1_blocks(st, _buf(blocks), len(blocks) // 64)
+    return list(st)
+
+
+def load_reference(opt="O2"):
+    """The reference's shahash from oracle/_ref (None when not built here)."""
+    path = REF_SO if opt == "O2" else REF_SO_O0
+    if not os.path.exists(path):
+        return None
+    ref = ctypes.CDLL(path)
+    ref.shahash.argtypes = [_vp, ctypes.c_int, _vp]
+    ref.shahash.restype = None
+    return ref

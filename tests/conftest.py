@@ -1,0 +1,54 @@
+"""Shared test plumbing.
+
+Markers: `gpu` = needs a real MI355X (run with `-m gpu` on the GPU box); every
+other test runs on CPU here.  The product binding (btsha1) is loaded from the
+package directory (its name has dashes, so by path); the oracle is the
+TEST-ONLY checker under oracle/.
+"""
+import importlib.util
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "bittorrent-with-congestion-control_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+
+
+def load_btsha1():
+    if "btsha1" in sys.modules:
+        return sys.modules["btsha1"]
+    spec = importlib.util.spec_from_file_location("btsha1", os.path.join(PKG, "btsha1.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["btsha1"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def read_pairs(name):
+    """'<a> <b> [<c>]' golden lines (comments skipped) as tuples of strings."""
+    rows = []
+    with open(os.path.join(GOLDEN, name)) as f:
+        for line in f:
+            if line.startswith("#") or not line.strip():
+                continue
+            rows.append(tuple(line.split()))
+    return rows
+
+
+def c_tar_bytes():
+    import lzma
+    with open(os.path.join(GOLDEN, "C.tar.xz"), "rb") as f:
+        return lzma.decompress(f.read())
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import py_oracle
+    return py_oracle

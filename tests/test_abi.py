@@ -1,0 +1,95 @@
+"""CPU: the C-ABI library builds, loads, exports every declared entry point,
+and fails loudly (not silently, not on the CPU) when no GPU is present."""
+import ctypes
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO, PKG, load_btsha1
+
+LIB = os.path.join(PKG, "libbtsha1.so")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("bt_sha1.h", "sha.h", "chunk.h")]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        text = re.sub(r"//[^\n]*", "", text)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", text, flags=re.M):
+            if not m.group(0).lstrip().startswith(("#", "typedef")):
+                names.add(m.group(1))
+    return names
+
+
+def test_headers_declare_reference_surface():
+    names = declared_functions()
+    # sha.h:58-60 and chunk.h:25-34 of the reference
+    for ref in ["SHA1Init", "SHA1Update", "SHA1Final", "make_chunks", "shahash", "binary2hex", "hex2binary"]:
+        assert ref in names
+    assert len(names) > 25
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB), "run make first"
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    missing = declared_functions() - exported
+    assert not missing, missing
+
+
+def test_library_is_gfx950_code_object():
+    blob = open(LIB, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"k_sha1_fixed" in blob
+
+
+def test_loads_and_reports_no_device_loudly():
+    bt = load_btsha1()
+    if bt.device_count() > 0:
+        pytest.skip("a GPU is visible; covered by the gpu tests")
+    with pytest.raises(bt.BtSha1Error, match="device"):
+        bt.chunks_host(b"x" * 100, 64)
+    assert "gfx950" in bt.build_info()
+
+
+def test_dropin_void_calls_abort_without_gpu(tmp_path):
+    """shahash cannot return an error (chunk.h:28): it must abort, never hash on the CPU."""
+    code = ("import ctypes,sys; l=ctypes.CDLL(sys.argv[1]); o=(ctypes.c_uint8*20)(); "
+            "l.shahash(b'abc', 3, o); print('returned', bytes(o).hex())")
+    r = subprocess.run([sys.executable, "-c", code, LIB], capture_output=True, text=True)
+    if "returned" in r.stdout and r.returncode == 0:
+        pytest.skip("GPU visible")
+    assert r.returncode != 0
+    assert "libbtsha1: shahash" in r.stderr
+
+
+def test_sha1context_layout_matches_reference():
+    bt = load_btsha1()
+    # sha.h:39-50 of the reference: u64 + 5*u32 + u32 + 64-byte union = 96 bytes
+    assert ctypes.sizeof(bt.SHA1Context) == 96
+    assert bt.SHA1Context.buffer.offset == 32
+
+
+def test_hex_codec_is_host_formatting():
+    bt = load_btsha1()
+    b = bytes(range(20))
+    assert bt.binary2hex(b) == b.hex()
+    assert bt.hex2binary(b.hex()) == b
+    assert bt.hex2binary("0g") == bytes([16])  # bug-compatible with chunk.c:66-71
+
+
+def test_reference_callers_compile_and_link_against_dropin(tmp_path):
+    """make_chunks.c and chunk-using code of the reference build unchanged
+    against include/ + libbtsha1.so (the drop-in claim)."""
+    src = "/root/reference/make_chunks.c"
+    if not os.path.exists(src):
+        pytest.skip("reference sources absent (GPU box)")
+    exe = tmp_path / "make-chunks-dropin"
+    subprocess.run(["gcc", "-Wall", "-I", os.path.join(REPO, "include"), "-o", str(exe), src,
+                    f"-L{PKG}", "-lbtsha1", "-lm", f"-Wl,-rpath,{PKG}"], check=True, capture_output=True)
+    assert exe.exists()

@@ -1,0 +1,303 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the
+reference's golden vectors.  Bit-exact everywhere (integer/byte work)."""
+import hashlib
+import os
+import random
+import subprocess
+
+import pytest
+
+from conftest import GOLDEN, PKG, REPO, c_tar_bytes, load_btsha1, read_pairs
+
+pytestmark = pytest.mark.gpu
+CHUNK = 512 * 1024
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "gpu tests need a HIP device"
+    return t
+
+
+@pytest.fixture(scope="module")
+def bt(torch):
+    m = load_btsha1()
+    assert m.device_count() >= 1
+    return m
+
+
+def to_dev(torch, data: bytes, pad=0):
+    t = torch.zeros(len(data) + pad + 16, dtype=torch.uint8, device="cuda")
+    if data:
+        t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    return t
+
+
+def digests_of(torch, t, n):
+    return [bytes(t[20 * i:20 * i + 20].cpu().numpy().tobytes()) for i in range(n)]
+
+
+def kat_data():
+    return {"abc": b"abc", "dash": b"dash", "empty": b"",
+            "nist448": b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq",
+            "zeros_512k": bytes(CHUNK), "ff_512k": b"\xff" * CHUNK,
+            "iota_512k": bytes(i & 255 for i in range(CHUNK)), "million_a": b"a" * 1000000}
+
+
+def test_shahash_kats(bt):
+    data = kat_data()
+    for name, n, h in read_pairs("kat.txt"):
+        assert bt.shahash(data[name]).hex() == h, name
+
+
+def test_streaming_api_kats_random_splits(bt):
+    data = kat_data()
+    rng = random.Random(1)
+    for name, n, h in read_pairs("kat.txt"):
+        d = data[name]
+        s = bt.Sha1()
+        i = 0
+        while i < len(d):
+            j = min(len(d), i + rng.choice([1, 3, 63, 64, 65, 640, 4096, 100000]))
+            s.update(d[i:j])
+            i = j
+        assert s.final().hex() == h, name
+
+
+def test_streaming_context_fields(bt, oracle):
+    s = bt.Sha1().update(b"x" * 100)
+    assert s.ctx.totalLength == 800 and s.ctx.bufferLength == 36
+    assert list(s.ctx.hash) == oracle.compress_blocks(
+        [0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476, 0xc3d2e1f0], b"x" * 64)
+
+
+def test_edge_lengths_ragged_kernel(bt, torch, oracle):
+    rows = read_pairs("edge_lengths.txt")
+    stream = bytes(oracle.fill_synthetic(max(int(n) for n, _ in rows), 0, oracle.SEED_EDGE))
+    d = to_dev(torch, stream)
+    n = len(rows)
+    offs = torch.zeros(n, dtype=torch.int64, device="cuda")
+    lens = torch.tensor([int(x) for x, _ in rows], dtype=torch.int32, device="cuda")
+    out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+    bt.ragged_dev(d.data_ptr(), offs.data_ptr(), lens.data_ptr(), n, out.data_ptr())
+    torch.cuda.synchronize()
+    assert [x.hex() for x in digests_of(torch, out, n)] == [h for _, h in rows]
+
+
+def test_ragged_golden_batch_unaligned(bt, torch, oracle):
+    rows = read_pairs("ragged.txt")
+    msgs = [bytes(oracle.fill_synthetic(int(n), int(k) * 1024, oracle.SEED_RAGGED)) for k, n, _ in rows]
+    # pack with deliberately odd offsets (1..7 bytes of slack) to hit every alignment
+    blob, offs = bytearray(), []
+    for i, m in enumerate(msgs):
+        blob += bytes(1 + i % 7)
+        offs.append(len(blob))
+        blob += m
+    d = to_dev(torch, bytes(blob))
+    o = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    l = torch.tensor([len(m) for m in msgs], dtype=torch.int32, device="cuda")
+    out = torch.zeros(20 * len(msgs), dtype=torch.uint8, device="cuda")
+    bt.ragged_dev(d.data_ptr(), o.data_ptr(), l.data_ptr(), len(msgs), out.data_ptr())
+    torch.cuda.synchronize()
+    assert [x.hex() for x in digests_of(torch, out, len(msgs))] == [h for _, _, h in rows]
+
+
+def test_device_generator_matches_oracle(bt, torch, oracle):
+    for nbytes, first in [(CHUNK, 7 * 65536), (1000, 3), (4096 + 8, 2**40 + 1)]:
+        t = torch.zeros(nbytes + 32, dtype=torch.uint8, device="cuda")
+        bt.fill_synthetic(t.data_ptr(), nbytes, first, oracle.SEED_SYNTH)
+        torch.cuda.synchronize()
+        assert bytes(t[:nbytes].cpu().numpy().tobytes()) == bytes(oracle.fill_synthetic(nbytes, first, oracle.SEED_SYNTH))
+        assert int(t[nbytes:].sum()) == 0  # no overrun
+
+
+@pytest.fixture(scope="module")
+def synth4096(bt, torch, oracle):
+    n = 4096
+    buf = torch.empty(n * CHUNK, dtype=torch.uint8, device="cuda")
+    bt.fill_synthetic(buf.data_ptr(), n * CHUNK, 0, oracle.SEED_SYNTH)
+    torch.cuda.synchronize()
+    return buf
+
+
+@pytest.mark.parametrize("ring", [2, 3, 4])
+def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, ring):
+    """BASELINE config 2: 4096 synthetic 512 KiB chunks, every digest == sha.c's."""
+    bt.set_ring_depth(ring)
+    try:
+        n = 4096
+        out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+        bt.chunks_dev(synth4096.data_ptr(), n, CHUNK, CHUNK, out.data_ptr())
+        torch.cuda.synchronize()
+        raw = out.cpu().numpy().tobytes()
+        got = [(str(i), raw[20 * i:20 * i + 20].hex()) for i in range(n)]
+        assert got == read_pairs("synth4096.txt")
+    finally:
+        bt.set_ring_depth(3)
+
+
+def test_verify_dev_flags_mismatches(bt, torch, synth4096):
+    n = 1000
+    golden = read_pairs("synth4096.txt")[:n]
+    exp = bytearray(b"".join(bytes.fromhex(h) for _, h in golden))
+    bad = {0, 17, 511, 999}
+    for i in bad:
+        exp[20 * i + (i % 20)] ^= 1
+    d_exp = to_dev(torch, bytes(exp))
+    ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    dig = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+    bt.verify_dev(synth4096.data_ptr(), n, CHUNK, CHUNK, d_exp.data_ptr(), ok.data_ptr(), dig.data_ptr())
+    torch.cuda.synchronize()
+    okl = ok.cpu().tolist()
+    assert [i for i, v in enumerate(okl) if v == 0] == sorted(bad)
+    assert all(v == 1 for i, v in enumerate(okl) if i not in bad)
+    assert digests_of(torch, dig, 3)[2].hex() == golden[2][1]
+
+
+@pytest.mark.parametrize("chunk_len,pitch,n", [
+    (0, 16, 5), (1, 16, 3), (55, 64, 65), (56, 64, 64), (64, 64, 63), (100, 112, 129),
+    (128, 128, 64), (192, 192, 65), (448, 448, 70), (4096 + 17, 4096 + 32, 130),
+    (65536 + 63, 65536 + 64, 66), (3 * 128 * 5, 3 * 128 * 5, 200),
+    (1000, 1003, 67),            # odd pitch -> generic kernel
+    (CHUNK, CHUNK + 256, 65),    # padded pitch, fast kernel
+])
+def test_fixed_layouts_vs_oracle(bt, torch, oracle, chunk_len, pitch, n):
+    total = pitch * (n - 1) + chunk_len
+    host = bytearray(oracle.fill_synthetic(total, 11, 0xC0FFEE))
+    d = to_dev(torch, bytes(host))
+    out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+    bt.chunks_dev(d.data_ptr(), n, chunk_len, pitch, out.data_ptr())
+    torch.cuda.synchronize()
+    want = [oracle.sha1(bytes(host[i * pitch:i * pitch + chunk_len])) for i in range(n)]
+    assert digests_of(torch, out, n) == want
+
+
+def test_every_ring_depth_on_ragged_line_counts(bt, torch, oracle):
+    for ring in (2, 3, 4):
+        bt.set_ring_depth(ring)
+        for blocks in range(0, 2 * 2 * ring + 3):
+            for r in (0, 5, 56):
+                L = 64 * blocks + r
+                n = 70
+                pitch = (L + 15) // 16 * 16 or 16
+                host = bytearray(oracle.fill_synthetic(pitch * n, blocks, ring))
+                d = to_dev(torch, bytes(host))
+                out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+                bt.chunks_dev(d.data_ptr(), n, L, pitch, out.data_ptr())
+                torch.cuda.synchronize()
+                got = digests_of(torch, out, n)
+                for i in (0, 1, 63, 64, 69):
+                    assert got[i] == oracle.sha1(bytes(host[i * pitch:i * pitch + L])), (ring, L, i)
+    bt.set_ring_depth(3)
+
+
+def test_host_pipeline_c_tar_and_tail(bt, oracle):
+    img = c_tar_bytes()
+    got = [d.hex() for d in bt.chunks_host(img)]
+    ref = [l.split()[1] for l in open(os.path.join(GOLDEN, "ref_C.chunks")).read().splitlines()[2:]]
+    assert got == ref
+    tail = bytes(oracle.fill_synthetic(3 * CHUNK + 12345, 0, oracle.SEED_TAIL))
+    want = open(os.path.join(GOLDEN, "tail.make-chunks.out")).read()
+    assert "".join(f"{i} {d.hex()}\n" for i, d in enumerate(bt.chunks_host(tail))) == want
+    assert "".join(f"{i} {d.hex()}\n" for i, d in enumerate(bt.chunks_host(tail, ndev=0))) == want
+    assert bt.chunks_host(b"") == []
+    # many batches through the double-buffered pipeline (small chunks -> many per batch)
+    big = bytes(oracle.fill_synthetic(5 * 1024 * 1024 + 77, 9, 9))
+    assert bt.chunks_host(big, chunk_len=4096) == oracle.hash_chunks(big, 4096)
+
+
+def test_make_chunks_file_api(bt, oracle, tmp_path):
+    p = tmp_path / "C.tar"
+    p.write_bytes(c_tar_bytes())
+    assert "".join(f"{i} {d.hex()}\n" for i, d in enumerate(bt.make_chunks_file(str(p)))) == \
+        open(os.path.join(GOLDEN, "C.tar.make-chunks.out")).read()
+    e = tmp_path / "empty"
+    e.write_bytes(b"")
+    assert bt.make_chunks_file(str(e)) == []
+
+
+def test_make_chunks_cli(tmp_path, oracle):
+    exe = os.path.join(PKG, "bin", "make-chunks")
+    p = tmp_path / "C.tar"
+    p.write_bytes(c_tar_bytes())
+    out = subprocess.run([exe, str(p)], capture_output=True, check=True).stdout.decode()
+    assert out == open(os.path.join(GOLDEN, "C.tar.make-chunks.out")).read()
+    out_g = subprocess.run([exe, "-g", "0", "-m", str(p)], capture_output=True, check=True).stdout.decode()
+    assert out_g == f"File: {p}\nChunks:\n" + out
+    t = tmp_path / "tail.bin"
+    t.write_bytes(bytes(oracle.fill_synthetic(3 * CHUNK + 12345, 0, oracle.SEED_TAIL)))
+    out_t = subprocess.run([exe, str(t)], capture_output=True, check=True).stdout.decode()
+    assert out_t == open(os.path.join(GOLDEN, "tail.make-chunks.out")).read()
+
+
+def test_reference_make_chunks_linked_to_dropin(tmp_path):
+    """The reference's own make_chunks.c, unchanged, linked against libbtsha1.so
+    (built in the build container into oracle/_ref/make-chunks-dropin)."""
+    exe = os.path.join(REPO, "oracle", "_ref", "make-chunks-dropin")
+    if not os.path.exists(exe):
+        pytest.skip("drop-in reference binary not built")
+    p = tmp_path / "C.tar"
+    p.write_bytes(c_tar_bytes())
+    env = dict(os.environ, LD_LIBRARY_PATH=PKG + ":" + os.environ.get("LD_LIBRARY_PATH", ""))
+    out = subprocess.run([exe, str(p)], capture_output=True, check=True, env=env).stdout.decode()
+    assert out == open(os.path.join(GOLDEN, "C.tar.make-chunks.out")).read()
+
+
+def test_verify_stream_cli(tmp_path):
+    exe = os.path.join(PKG, "bin", "verify-stream")
+    p = tmp_path / "C.tar"
+    p.write_bytes(c_tar_bytes())
+    ck = os.path.join(GOLDEN, "ref_C.chunks")
+    r = subprocess.run([exe, "-b", "3", str(p), ck], capture_output=True, text=True, check=True)
+    assert '"ok": 4, "failed": 0' in r.stdout and "Verification failed" not in r.stdout
+    r = subprocess.run([exe, "-b", "2", "-x", str(p), ck], capture_output=True, text=True, check=True)
+    assert r.stdout.count("Verification failed!") == 1 and '"failed": 1' in r.stdout
+
+
+def test_verifier_async_batches(bt, oracle):
+    img = c_tar_bytes()
+    chunks = [img[i * CHUNK:(i + 1) * CHUNK] for i in range(4)]
+    ref = [bytes.fromhex(l.split()[1]) for l in open(os.path.join(GOLDEN, "ref_C.chunks")).read().splitlines()[2:]]
+    v = bt.Verifier(batch=5, nstreams=2)
+    results, want = [], []
+    for k in range(23):
+        exp = ref[k % 4] if k % 6 else bytes(20)  # every 6th expectation is wrong
+        if k % 2:
+            v.submit(chunks[k % 4], exp, tag=1000 + k)
+        else:
+            v.slot_fill(chunks[k % 4], exp, tag=1000 + k)
+        want.append((1000 + k, k % 6 != 0, ref[k % 4]))
+        results += v.poll()
+    results += v.drain()
+    assert v.pending() == 0
+    assert results == want
+    with pytest.raises(bt.BtSha1Error):
+        v.submit(b"short", ref[0], tag=1)
+    v.close()
+
+
+def test_full_size_config3_properties(bt, torch, oracle):
+    """BASELINE config 3 size (131072 x 512 KiB = 64 GiB in HBM): spot parity
+    against the oracle on regenerated host data, determinism, distinctness."""
+    n = 131072
+    try:
+        buf = torch.empty(n * CHUNK, dtype=torch.uint8, device="cuda")
+    except RuntimeError:
+        pytest.skip("not enough device memory")
+    bt.fill_synthetic(buf.data_ptr(), n * CHUNK, 0, oracle.SEED_SYNTH)
+    out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+    bt.chunks_dev(buf.data_ptr(), n, CHUNK, CHUNK, out.data_ptr())
+    out2 = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+    bt.chunks_dev(buf.data_ptr(), n, CHUNK, CHUNK, out2.data_ptr())
+    torch.cuda.synchronize()
+    del buf
+    raw = out.cpu().numpy().tobytes()
+    assert raw == out2.cpu().numpy().tobytes()
+    dig = [raw[20 * i:20 * i + 20] for i in range(n)]
+    assert len(set(dig)) == n
+    golden = read_pairs("synth4096.txt")
+    assert [d.hex() for d in dig[:4096]] == [h for _, h in golden]
+    sample = list(range(n - 64, n)) + list(range(4096, n, 1024))
+    for i in sample:
+        assert dig[i] == oracle.sha1(bytes(oracle.fill_synthetic(CHUNK, i * 65536, oracle.SEED_SYNTH))), i

@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--chunks", type=int, default=131072, help="512 KiB chunks per GPU")
     ap.add_argument("--ring", type=int, default=0, help="kernel ring depth (0 = library default)")
+    ap.add_argument("--lines", type=int, default=1, help="128-byte lines per ring slot (with --ring)")
+    ap.add_argument("--nt", type=int, default=0, help="non-temporal loads (with --ring)")
     ap.add_argument("--pitch", type=int, default=CHUNK, help="bytes between chunk starts in HBM")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-chunks", type=int, default=8192)
@@ -122,14 +124,18 @@ def main():
         cpu_group = dist.new_group(backend="gloo")
     bt = load_btsha1()
     if args.ring:
-        bt.set_ring_depth(args.ring)
+        bt.set_variant(args.ring, args.lines, args.nt)
 
     C = args.chunks
     pitch = args.pitch
     buf = torch.empty(pitch * (C - 1) + CHUNK + 256, dtype=torch.uint8, device="cuda")
     dig = torch.zeros(20 * C, dtype=torch.uint8, device="cuda")
-    stream = torch.cuda.current_stream()
+    # A dedicated stream (torch's default stream has handle 0, which the C-ABI
+    # reads as "library stream"): kernels and timing events share it.
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
+    assert sp != 0
     first_chunk = rank * C
     if pitch == CHUNK:
         bt.fill_synthetic(buf.data_ptr(), C * CHUNK, first_chunk * (CHUNK // 8), SEED, sp)
@@ -236,7 +242,7 @@ def main():
             "chunks_per_gpu": C, "chunk_bytes": CHUNK, "pitch_bytes": pitch,
             "global_chunks": world * C,
             "parallelism": f"dp{world} (contiguous chunk-range split, no data-path collective)",
-            "ring_depth": bt.build_info().split("ring=")[-1],
+            "kernel_variant": bt.build_info().split("hip")[-1].split(" ", 1)[-1],
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

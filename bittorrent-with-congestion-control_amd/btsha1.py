@@ -52,11 +52,14 @@ _sig("bt_sha1_set_device", ctypes.c_int, ctypes.c_int)
 _sig("bt_sha1_last_error", ctypes.c_char_p)
 _sig("bt_sha1_build_info", ctypes.c_char_p)
 _sig("bt_sha1_set_ring_depth", ctypes.c_int, ctypes.c_int)
+_sig("bt_sha1_set_variant", ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int)
 _sig("bt_sha1_chunks_dev", ctypes.c_int, _vp, _u64, _u64, _u64, _vp, _vp)
 _sig("bt_sha1_verify_dev", ctypes.c_int, _vp, _u64, _u64, _u64, _vp, _vp, _vp, _vp)
 _sig("bt_sha1_ragged_dev", ctypes.c_int, _vp, _vp, _vp, _u64, _vp, _vp)
 _sig("bt_sha1_fill_synthetic", ctypes.c_int, _vp, _u64, _u64, _u64, _vp)
 _sig("bt_sha1_chunks_host", _i64, _vp, _u64, _u64, _vp)
+_sig("bt_sha1_host_register", ctypes.c_int, _vp, _u64)
+_sig("bt_sha1_host_unregister", ctypes.c_int, _vp)
 _sig("bt_sha1_chunks_host_multi", _i64, _vp, _u64, _u64, _vp, ctypes.c_int)
 _sig("bt_sha1_chunks_file", _i64, _vp, _u64, _vp, _u64)
 _sig("bt_sha1_verifier_create", _vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32)
@@ -92,6 +95,10 @@ def device_count():
 
 def set_ring_depth(nbuf):
     _check(lib.bt_sha1_set_ring_depth(nbuf), "set_ring_depth")
+
+
+def set_variant(nbuf, lines=1, nt=0):
+    _check(lib.bt_sha1_set_variant(nbuf, lines, nt), "set_variant")
 
 
 def build_info():
@@ -138,6 +145,26 @@ def chunks_host(data, chunk_len=CHUNK, ndev=None):
         got = _check(lib.bt_sha1_chunks_host_multi(buf, n, chunk_len, out, ndev), "bt_sha1_chunks_host_multi")
     raw = bytes(out)
     return [raw[20 * i:20 * i + 20] for i in range(got)]
+
+
+def host_register(addr, nbytes):
+    """Page-lock host memory at integer address `addr` (DMA without staging)."""
+    _check(lib.bt_sha1_host_register(addr, nbytes), "bt_sha1_host_register")
+
+
+def host_unregister(addr):
+    _check(lib.bt_sha1_host_unregister(addr), "bt_sha1_host_unregister")
+
+
+def chunks_host_addr(addr, nbytes, chunk_len=CHUNK, ndev=None):
+    """bt_sha1_chunks_host over raw host memory at `addr` (no copy on the Python side)."""
+    nch = (nbytes + chunk_len - 1) // chunk_len
+    out = (ctypes.c_uint8 * max(20 * nch, 1))()
+    if ndev is None:
+        got = _check(lib.bt_sha1_chunks_host(addr, nbytes, chunk_len, out), "bt_sha1_chunks_host")
+    else:
+        got = _check(lib.bt_sha1_chunks_host_multi(addr, nbytes, chunk_len, out, ndev), "bt_sha1_chunks_host_multi")
+    return bytes(out)[:20 * got]
 
 
 def shahash(data):

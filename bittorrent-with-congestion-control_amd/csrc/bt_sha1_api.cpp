@@ -26,6 +26,8 @@
 #include <thread>
 #include <vector>
 
+#include <sys/stat.h>
+
 #include "bt_sha1.h"
 #include "chunk.h"
 #include "sha1_launch.h"
@@ -34,7 +36,7 @@ namespace {
 
 thread_local std::string t_err;
 thread_local int t_dev = 0;
-std::atomic<int> g_nbuf{3};
+std::atomic<int> g_variant{310};  // ring 3 x 128-byte slots, default cache policy
 
 void set_err(const char *fmt, ...) {
   char buf[512];
@@ -164,7 +166,7 @@ bool fast_layout(const void *d_in, uint64_t chunk_len, uint64_t pitch, const voi
 int launch_chunks(const void *d_in, uint64_t n, uint64_t len, uint64_t pitch, uint8_t *d_dig, hipStream_t s) {
   if (n == 0) return 0;
   if (fast_layout(d_in, len, pitch, d_dig)) {
-    BT_CK(btsha1_launch_fixed(d_in, n, (uint32_t)pitch, (uint32_t)len, d_dig, nullptr, nullptr, s, g_nbuf.load()));
+    BT_CK(btsha1_launch_fixed(d_in, n, (uint32_t)pitch, (uint32_t)len, d_dig, nullptr, nullptr, s, g_variant.load()));
   } else {
     if (len >= (1ull << 32)) {
       set_err("chunk_len %llu exceeds 4 GiB", (unsigned long long)len);
@@ -185,25 +187,42 @@ int launch_image(const uint8_t *d_img, uint64_t bytes, uint64_t chunk_len, uint8
   return 0;
 }
 
-uint64_t batch_chunks_for(uint64_t chunk_len) {
-  const uint64_t target = 256ull << 20;  // bytes per staging buffer
-  return std::max<uint64_t>(1, target / chunk_len);
+// Staging batch: ~1 GiB per lane keeps >= 2048 chunks in flight per launch,
+// enough that the per-chunk hash latency (~10 ms, 8193 dependent blocks at one
+// wave per SIMD) still outruns PCIe; capped by the input size when known.
+uint64_t batch_bytes_for(uint64_t chunk_len, uint64_t size_hint) {
+  const uint64_t target = 1ull << 30;
+  uint64_t per = std::max<uint64_t>(1, target / chunk_len);
+  if (size_hint != UINT64_MAX) per = std::max<uint64_t>(1, std::min<uint64_t>(per, (size_hint + chunk_len - 1) / chunk_len));
+  return per * chunk_len;
 }
 
-// Generic double-buffered pipeline: fill(lane, first_chunk, max_bytes) puts
-// up to max_bytes of the image into lane.h_in and returns the byte count
-// (< max_bytes only at the end); sink(first_chunk, count, digests) receives
-// digests in chunk order.
+// Host memory the DMA engine can read directly (hipHostMalloc'd or
+// registered with bt_sha1_host_register): no staging copy needed.
+bool is_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// Generic double-buffered pipeline over two streams: batch k+1's H2D overlaps
+// batch k's hashing.  fill(lane, max_bytes, &src) provides up to max_bytes of
+// the image (in lane.h_in, or in place when already pinned) and returns the
+// byte count (< max_bytes only at the end); sink(first_chunk, count, digests)
+// receives digests in chunk order.
 template <class Fill, class Sink>
-int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, Fill fill, Sink sink) {
+int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool staged, Fill fill, Sink sink) {
   if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
     set_err("chunk_len must be in [1, 4 GiB)");
     return -1;
   }
-  const uint64_t per = batch_chunks_for(chunk_len);
-  const uint64_t bytes_per = per * chunk_len;
+  const uint64_t bytes_per = batch_bytes_for(chunk_len, size_hint);
+  const uint64_t per = bytes_per / chunk_len;
   for (auto &l : c->lane) {
-    if (l.h_in.ensure(bytes_per) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per) ||
+    if ((staged && l.h_in.ensure(bytes_per)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per) ||
         l.d_dig.ensure(20 * per))
       return -1;
     l.busy = false;
@@ -220,11 +239,12 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, Fill fill, Sink sink) {
   for (;;) {
     Lane &l = c->lane[k & 1];
     if (drain(l)) return -1;
-    int64_t got = fill(l, next, bytes_per);
+    const uint8_t *src = nullptr;
+    int64_t got = fill(l, bytes_per, &src);
     if (got < 0) return -1;
     if (got == 0) break;
     const uint64_t cnt = ((uint64_t)got + chunk_len - 1) / chunk_len;
-    BT_CK(hipMemcpyAsync(l.d_in.p, l.h_in.p, (size_t)got, hipMemcpyHostToDevice, l.s));
+    BT_CK(hipMemcpyAsync(l.d_in.p, src, (size_t)got, hipMemcpyHostToDevice, l.s));
     if (launch_image(l.d_in.as<uint8_t>(), (uint64_t)got, chunk_len, l.d_dig.as<uint8_t>(), l.s)) return -1;
     BT_CK(hipMemcpyAsync(l.h_dig.p, l.d_dig.p, 20 * cnt, hipMemcpyDeviceToHost, l.s));
     BT_CK(hipEventRecord(l.ev, l.s));
@@ -248,15 +268,21 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
     set_err("hipSetDevice(%d) failed", dev);
     return -1;
   }
+  const bool pinned = is_pinned(h_in);
   uint64_t off = 0;
-  auto fill = [&](Lane &l, uint64_t, uint64_t max) -> int64_t {
+  auto fill = [&](Lane &l, uint64_t max, const uint8_t **src) -> int64_t {
     const uint64_t n = std::min<uint64_t>(max, total - off);
-    memcpy(l.h_in.p, h_in + off, n);
+    if (pinned) {
+      *src = h_in + off;  // DMA straight from the caller's pinned image
+    } else {
+      memcpy(l.h_in.p, h_in + off, n);
+      *src = l.h_in.as<uint8_t>();
+    }
     off += n;
     return (int64_t)n;
   };
   auto sink = [&](uint64_t first, uint64_t count, const uint8_t *d) { memcpy(h_dig + 20 * first, d, 20 * count); };
-  return run_pipeline(c, chunk_len, fill, sink);
+  return run_pipeline(c, chunk_len, total, !pinned, fill, sink);
 }
 
 template <class Sink>
@@ -268,7 +294,12 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
     set_err("hipSetDevice(%d) failed", dev);
     return -1;
   }
-  auto fill = [&](Lane &l, uint64_t, uint64_t max) -> int64_t {
+  uint64_t hint = UINT64_MAX;
+  struct stat st;
+  const long pos = ftell(fp);
+  if (fstat(fileno(fp), &st) == 0 && S_ISREG(st.st_mode) && pos >= 0 && st.st_size >= pos)
+    hint = (uint64_t)(st.st_size - pos);
+  auto fill = [&](Lane &l, uint64_t max, const uint8_t **src) -> int64_t {
     // fread straight into pinned memory; short only at EOF (chunk.c:20).
     size_t got = 0;
     while (got < max) {
@@ -280,9 +311,10 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
       set_err("fread failed");
       return -1;
     }
+    *src = l.h_in.as<uint8_t>();
     return (int64_t)got;
   };
-  return run_pipeline(c, chunk_len, fill, sink);
+  return run_pipeline(c, chunk_len, hint, true, fill, sink);
 }
 
 // Single message on the GPU (shahash): stage, ragged kernel, 20 bytes back.
@@ -349,16 +381,19 @@ const char *bt_sha1_last_error(void) { return t_err.c_str(); }
 const char *bt_sha1_build_info(void) {
   static char info[128];
   snprintf(info, sizeof info, "libbtsha1 gfx950 hip%d.%d ring=%d", HIP_VERSION_MAJOR, HIP_VERSION_MINOR,
-           g_nbuf.load());
+           g_variant.load());
   return info;
 }
 
-int bt_sha1_set_ring_depth(int nbuf) {
-  if (nbuf < 2 || nbuf > 4) {
-    set_err("ring depth must be 2, 3 or 4");
+int bt_sha1_set_ring_depth(int nbuf) { return bt_sha1_set_variant(nbuf, 1, 0); }
+
+int bt_sha1_set_variant(int nbuf, int lines, int nt) {
+  const int code = nbuf * 100 + lines * 10 + (nt ? 1 : 0);
+  if (!btsha1_fixed_variant_ok(code)) {
+    set_err("no hot-kernel variant ring=%d lines=%d nt=%d", nbuf, lines, nt);
     return -1;
   }
-  g_nbuf.store(nbuf);
+  g_variant.store(code);
   return 0;
 }
 
@@ -396,7 +431,7 @@ int bt_sha1_verify_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
   BT_CK(btsha1_launch_fixed(d_in, n, (uint32_t)pitch, (uint32_t)chunk_len, d_digests, d_expected, d_ok,
-                            pick_stream(stream, c), g_nbuf.load()));
+                            pick_stream(stream, c), g_variant.load()));
   return 0;
 }
 
@@ -425,6 +460,21 @@ int bt_sha1_fill_synthetic(void *d_buf, uint64_t nbytes, uint64_t first_word, ui
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
   BT_CK(btsha1_launch_fill(d_buf, nbytes, first_word, seed, pick_stream(stream, c)));
+  return 0;
+}
+
+int bt_sha1_host_register(void *h_ptr, uint64_t len) {
+  if (!h_ptr || !len) {
+    set_err("null pointer or zero length");
+    return -1;
+  }
+  if (!ctx_for(t_dev)) return -1;
+  BT_CK(hipHostRegister(h_ptr, (size_t)len, hipHostRegisterPortable));
+  return 0;
+}
+
+int bt_sha1_host_unregister(void *h_ptr) {
+  BT_CK(hipHostUnregister(h_ptr));
   return 0;
 }
 
@@ -678,7 +728,7 @@ int v_launch(bt_sha1_verifier *v) {
   BT_CK(hipMemcpyAsync(b.d_in, b.h_in, bytes, hipMemcpyHostToDevice, b.s));
   BT_CK(hipMemcpyAsync(b.d_exp, b.h_exp, 20 * (size_t)b.count, hipMemcpyHostToDevice, b.s));
   BT_CK(btsha1_launch_fixed(b.d_in, b.count, v->chunk_len, v->chunk_len, b.d_dig, b.d_exp, b.d_ok, b.s,
-                            g_nbuf.load()));
+                            g_variant.load()));
   BT_CK(hipMemcpyAsync(b.h_ok, b.d_ok, b.count, hipMemcpyDeviceToHost, b.s));
   BT_CK(hipMemcpyAsync(b.h_dig, b.d_dig, 20 * (size_t)b.count, hipMemcpyDeviceToHost, b.s));
   BT_CK(hipEventRecord(b.ev, b.s));

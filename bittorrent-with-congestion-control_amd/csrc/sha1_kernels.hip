@@ -31,27 +31,31 @@ constexpr int kBlock = 256;  // 4 waves; 2 blocks per CU at 131072 chunks
 // ---------------------------------------------------------------------------
 // Hot path.
 // ---------------------------------------------------------------------------
-template <int NBUF>
-__device__ __forceinline__ void load_line(u32x4 (&q)[8], __amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
+// One ring slot = L consecutive 128-byte lines of the lane's own chunk
+// (2L SHA-1 blocks), fetched as 8L back-to-back 16-byte buffer loads so the
+// DRAM sees one L*128-byte burst per chunk per slot.
+template <int L, int AUX>
+__device__ __forceinline__ void load_slot(u32x4 (&q)[8 * L], __amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
                                           uint32_t soff) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) q[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff + 16 * j, 0);
+  for (int j = 0; j < 8 * L; ++j) q[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff + 16 * j, AUX);
 }
 
-__device__ __forceinline__ void compress_line(State &st, const u32x4 (&q)[8]) {
-  uint32_t w[16];
-  block_from_le(w, q[0], q[1], q[2], q[3]);
-  compress(st, w);
-  block_from_le(w, q[4], q[5], q[6], q[7]);
-  compress(st, w);
+template <int L>
+__device__ __forceinline__ void compress_slot(State &st, const u32x4 (&q)[8 * L]) {
+#pragma unroll
+  for (int b = 0; b < 2 * L; ++b) {
+    uint32_t w[16];
+    block_from_le(w, q[4 * b], q[4 * b + 1], q[4 * b + 2], q[4 * b + 3]);
+    compress(st, w);
+  }
 }
 
-template <int NBUF, bool VERIFY>
-__global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sha1_fixed(const uint8_t *__restrict__ base, uint64_t n_chunks,
-                                                          uint32_t pitch, uint32_t len,
-                                                          uint8_t *__restrict__ digests,
-                                                          const uint8_t *__restrict__ expected,
-                                                          uint8_t *__restrict__ ok) {
+// NBUF ring slots of L lines; AUX = buffer-load cache policy (0 default, 2 nt).
+template <int NBUF, int L, int AUX, bool VERIFY>
+__global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sha1_fixed(
+    const uint8_t *__restrict__ base, uint64_t n_chunks, uint32_t pitch, uint32_t len, uint8_t *__restrict__ digests,
+    const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t chunk0 = (uint64_t)blockIdx.x * kBlock + (uint64_t)wave * 64u;  // wave-uniform
@@ -67,30 +71,31 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
 
   State st;
   st.init();
+  constexpr uint32_t kSlot = 128u * L;
   const uint32_t nblocks = len >> 6;
-  const uint32_t nlines = nblocks >> 1;
-  const uint32_t nmain = (nlines / NBUF) * NBUF;  // lines covered by the pipelined loop
+  const uint32_t nslots = nblocks / (2u * L);
+  const uint32_t nmain = (nslots / NBUF) * NBUF;  // slots covered by the pipelined loop
 
   if (nmain) {
-    u32x4 ring[NBUF][8];
+    u32x4 ring[NBUF][8 * L];
 #pragma unroll
-    for (int i = 0; i < NBUF - 1; ++i) load_line<NBUF>(ring[i], rsrc, voff, (uint32_t)i * 128u);
-    for (uint32_t line = 0; line < nmain; line += NBUF) {
+    for (int i = 0; i < NBUF - 1; ++i) load_slot<L, AUX>(ring[i], rsrc, voff, (uint32_t)i * kSlot);
+    for (uint32_t slot = 0; slot < nmain; slot += NBUF) {
 #pragma unroll
       for (int s = 0; s < NBUF; ++s) {
-        // Prefetch may run NBUF-1 lines past the chunk: it reads the next
+        // Prefetch may run NBUF-1 slots past the chunk: it reads the next
         // chunk's bytes or, past nrec, range-checked zeros; never used.
-        load_line<NBUF>(ring[(s + NBUF - 1) % NBUF], rsrc, voff, (line + s + NBUF - 1) * 128u);
+        load_slot<L, AUX>(ring[(s + NBUF - 1) % NBUF], rsrc, voff, (slot + s + NBUF - 1) * kSlot);
         // Pin the prefetch here: left alone, the scheduler sinks it to the
         // loop end to cut register pressure and the ring degenerates into a
         // vmcnt(0) at the loop head.
         __builtin_amdgcn_sched_barrier(0);
-        compress_line(st, ring[s]);
+        compress_slot<L>(st, ring[s]);
       }
     }
   }
-  // Remaining whole blocks (at most 2*NBUF-1 of them), loaded directly.
-  for (uint32_t b = nmain * 2; b < nblocks; ++b) {
+  // Remaining whole blocks (fewer than 2*L*NBUF), loaded directly.
+  for (uint32_t b = nmain * 2u * L; b < nblocks; ++b) {
     uint32_t w[16];
     const uint32_t o = b * 64u;
     block_from_le(w, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o, 0),
@@ -245,27 +250,38 @@ __global__ __launch_bounds__(kBlock) void k_fill_synthetic(uint8_t *__restrict__
 // ---------------------------------------------------------------------------
 using namespace btsha1;
 
-template <int NBUF>
-static hipError_t launch_fixed_nbuf(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
-                                    const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s) {
+template <int NBUF, int L, int AUX>
+static hipError_t launch_fixed_v(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
+                                 const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s) {
   const uint64_t grid = (n + kBlock - 1) / kBlock;
   if (d_ok)
-    hipLaunchKernelGGL((k_sha1_fixed<NBUF, true>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, true>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
                        (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok);
   else
-    hipLaunchKernelGGL((k_sha1_fixed<NBUF, false>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, false>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
                        (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok);
   return hipGetLastError();
 }
 
+// Variant code: NBUF*100 + L*10 + (nt ? 1 : 0).
+#define BT_FIXED_VARIANTS(X) X(2, 1, 0) X(3, 1, 0) X(4, 1, 0) X(2, 2, 0) \
+  X(2, 1, 2) X(3, 1, 2) X(2, 2, 2)
+
+bool btsha1_fixed_variant_ok(int code) {
+#define BT_CASE(N, L, A) if (code == N * 100 + L * 10 + (A ? 1 : 0)) return true;
+  BT_FIXED_VARIANTS(BT_CASE)
+#undef BT_CASE
+  return false;
+}
+
 hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
-                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int nbuf) {
+                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant) {
   if (n == 0) return hipSuccess;
-  switch (nbuf) {
-    case 2: return launch_fixed_nbuf<2>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
-    case 4: return launch_fixed_nbuf<4>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
-    default: return launch_fixed_nbuf<3>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
-  }
+#define BT_CASE(N, L, A) \
+  if (variant == N * 100 + L * 10 + (A ? 1 : 0)) return launch_fixed_v<N, L, A>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
+  BT_FIXED_VARIANTS(BT_CASE)
+#undef BT_CASE
+  return hipErrorInvalidValue;
 }
 
 hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t pitch,

@@ -8,7 +8,9 @@
 // d_in 16-byte aligned.  d_dig: 20*n bytes (4-byte aligned) or NULL.  When
 // d_ok != NULL also compares against d_exp (20*n) and writes one byte per chunk.
 hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
-                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int nbuf);
+                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant);
+// Hot-kernel variant code = ring slots*100 + lines per slot*10 + nt flag.
+bool btsha1_fixed_variant_ok(int code);
 // n messages at d_base + d_off[i], d_len[i] bytes each; with d_off == NULL,
 // message i is at d_base + i*pitch, fixed_len bytes.  Any alignment.
 hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t pitch,

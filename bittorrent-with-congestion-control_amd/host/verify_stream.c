@@ -2,7 +2,7 @@
  * verify-stream -- the received-chunk verify path of the peer (util.c:250-337)
  * driven through the batched GPU verifier, end to end from host memory.
  *
- *   verify-stream [-b batch] [-s streams] [-r rounds] [-x] <data-file> <chunks-file>
+ *   verify-stream [-b batch] [-s streams] [-r rounds] [-x] [-z] <data-file> <chunks-file>
  *
  * For every chunk listed in <chunks-file> ("<id> <hex>" lines, as
  * parse_has_get_chunk_file reads them, util.c:90-93) the chunk's bytes are
@@ -12,8 +12,12 @@
  * (util.c:311-313 becomes a batched GPU verify).  Verdicts are polled from the
  * loop like a select() tick would.  A failed chunk prints "Verification
  * failed!" exactly as util.c:317-318 does.  -x flips one byte of every 7th
- * chunk to exercise the failure branch.  The last line is a JSON summary with
- * the host->verdict rate.
+ * chunk to exercise the failure branch.  -z ("zero-copy receive") models a
+ * receiver that lands DATA payloads directly in the pinned slots (recvfrom
+ * into bt_sha1_verifier_slot() + offset): slots are written once, then every
+ * later commit re-verifies the bytes already resident in its slot, so the
+ * measured rate is the H2D + hash + D2H pipeline alone.  The last line is a
+ * JSON summary with the host->verdict rate.
  */
 #include <fcntl.h>
 #include <stdio.h>
@@ -36,12 +40,13 @@ static double now(void) {
 }
 
 int main(int argc, char **argv) {
-  int batch = 64, streams = 2, rounds = 1, corrupt = 0, opt;
-  while ((opt = getopt(argc, argv, "b:s:r:x")) != -1) {
+  int batch = 64, streams = 2, rounds = 1, corrupt = 0, zcopy = 0, opt;
+  while ((opt = getopt(argc, argv, "b:s:r:xz")) != -1) {
     if (opt == 'b') batch = atoi(optarg);
     else if (opt == 's') streams = atoi(optarg);
     else if (opt == 'r') rounds = atoi(optarg);
     else if (opt == 'x') corrupt = 1;
+    else if (opt == 'z') zcopy = 1;
     else {
       fprintf(stderr, "usage: %s [-b batch] [-s streams] [-r rounds] [-x] <data-file> <chunks-file>\n", argv[0]);
       return 255;
@@ -86,23 +91,43 @@ int main(int argc, char **argv) {
     fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
     return 255;
   }
+  /* only whole chunks are verified (util.c:307) */
+  int m0 = 0;
+  for (int k = 0; k < n; k++)
+    if ((uint64_t)ids[k] * BT_CHUNK_SIZE + BT_CHUNK_SIZE <= (uint64_t)st.st_size) {
+      ids[m0] = ids[k];
+      memcpy(exp + 20 * m0, exp + 20 * k, 20);
+      m0++;
+    }
+  n = m0;
+  const long ring = (long)batch * (streams < 2 ? 2 : streams);
+  long per_round = n;
+  if (zcopy) {
+    if (n == 0 || ring % n) {
+      fprintf(stderr, "verify-stream -z: batch*streams (%ld) must be a multiple of the chunk count (%d)\n", ring, n);
+      return 255;
+    }
+    per_round = ring;
+  }
   bt_sha1_verdict out[256];
   long good = 0, bad = 0, total = 0;
   double t0 = now();
   for (int r = 0; r < rounds; r++) {
-    for (int k = 0; k < n; k++) {
+    for (long i = 0; i < per_round; i++) {
+      const int k = (int)(i % n);
       const uint64_t off = (uint64_t)ids[k] * BT_CHUNK_SIZE;
-      if (off + BT_CHUNK_SIZE > (uint64_t)st.st_size) continue; /* only whole chunks are verified (util.c:307) */
       uint8_t *slot = bt_sha1_verifier_slot(v);
       if (!slot) {
         fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
         return 255;
       }
-      for (uint32_t got = 0; got < BT_CHUNK_SIZE; got += PAYLOAD) { /* save_data_packet, util.c:275 */
-        uint32_t len = BT_CHUNK_SIZE - got < PAYLOAD ? BT_CHUNK_SIZE - got : PAYLOAD;
-        memcpy(slot + got, img + off + got, len);
+      if (!zcopy || r == 0) {
+        for (uint32_t got = 0; got < BT_CHUNK_SIZE; got += PAYLOAD) { /* save_data_packet, util.c:275 */
+          uint32_t len = BT_CHUNK_SIZE - got < PAYLOAD ? BT_CHUNK_SIZE - got : PAYLOAD;
+          memcpy(slot + got, img + off + got, len);
+        }
+        if (corrupt && k % 7 == 3) slot[k % BT_CHUNK_SIZE] ^= 0x5a;
       }
-      if (corrupt && k % 7 == 3) slot[k % BT_CHUNK_SIZE] ^= 0x5a;
       if (bt_sha1_verifier_commit(v, BT_CHUNK_SIZE, exp + 20 * k, (uint64_t)k)) {
         fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
         return 255;
@@ -134,7 +159,8 @@ int main(int argc, char **argv) {
     }
   double dt = now() - t0;
   bt_sha1_verifier_destroy(v);
-  printf("{\"chunks\": %ld, \"ok\": %ld, \"failed\": %ld, \"seconds\": %.6f, \"GiB_per_s\": %.4f, \"batch\": %d, \"streams\": %d}\n",
-         total, good, bad, dt, total * (double)BT_CHUNK_SIZE / dt / (1u << 30), batch, streams);
+  printf("{\"chunks\": %ld, \"ok\": %ld, \"failed\": %ld, \"seconds\": %.6f, \"GiB_per_s\": %.4f, \"batch\": %d, \"streams\": %d, \"mode\": \"%s\"}\n",
+         total, good, bad, dt, total * (double)BT_CHUNK_SIZE / dt / (1u << 30), batch, streams,
+         zcopy ? "zero-copy slots" : "packetized memcpy (util.c:275)");
   return bad && !corrupt ? 1 : 0;
 }

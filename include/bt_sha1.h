@@ -48,6 +48,9 @@ const char *bt_sha1_last_error(void);
 const char *bt_sha1_build_info(void);
 /* Hot-kernel register-ring depth in 128-byte lines (2, 3 or 4; default 3). */
 int bt_sha1_set_ring_depth(int nbuf);
+/* Hot-kernel variant: nbuf ring slots of `lines` 128-byte lines each, nt = 1
+ * for non-temporal loads.  Returns -1 for a combination not compiled in. */
+int bt_sha1_set_variant(int nbuf, int lines, int nt);
 
 /* ---- device-resident batches (the hot path) ---------------------------- */
 /* n chunks of chunk_len bytes, chunk i at d_in + i*pitch (pitch >= chunk_len).
@@ -69,6 +72,10 @@ int bt_sha1_fill_synthetic(void *d_buf, uint64_t nbytes, uint64_t first_word, ui
                            void *stream);
 
 /* ---- host batches (H2D -> kernel -> D2H, double-buffered pinned staging) - */
+/* Page-lock a caller buffer (e.g. an mmap'ed file or a receive ring) so the
+ * host batch calls DMA from it directly instead of copying into staging. */
+int bt_sha1_host_register(void *h_ptr, uint64_t len);
+int bt_sha1_host_unregister(void *h_ptr);
 /* make_chunks over a memory image: chunk i = h_in[i*chunk_len ..], the last
  * one may be short.  Returns the chunk count (ceil(total_len/chunk_len)). */
 int64_t bt_sha1_chunks_host(const void *h_in, uint64_t total_len, uint64_t chunk_len,

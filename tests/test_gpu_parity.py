@@ -301,3 +301,26 @@ def test_full_size_config3_properties(bt, torch, oracle):
     sample = list(range(n - 64, n)) + list(range(4096, n, 1024))
     for i in sample:
         assert dig[i] == oracle.sha1(bytes(oracle.fill_synthetic(CHUNK, i * 65536, oracle.SEED_SYNTH))), i
+
+
+def test_registered_host_image_direct_dma(bt, oracle):
+    import numpy as np
+    data = np.frombuffer(bytes(oracle.fill_synthetic(9 * CHUNK + 777, 5, 0xD1A), ), dtype=np.uint8).copy()
+    want = b"".join(oracle.hash_chunks(bytes(data), CHUNK))
+    addr = data.ctypes.data
+    assert bt.chunks_host_addr(addr, data.nbytes) == want          # pageable: staged
+    bt.host_register(addr, data.nbytes)
+    try:
+        assert bt.chunks_host_addr(addr, data.nbytes) == want      # pinned: direct DMA
+        assert bt.chunks_host_addr(addr, data.nbytes, ndev=0) == want
+    finally:
+        bt.host_unregister(addr)
+
+
+def test_verify_stream_zero_copy_mode(tmp_path):
+    exe = os.path.join(PKG, "bin", "verify-stream")
+    p = tmp_path / "C.tar"
+    p.write_bytes(c_tar_bytes())
+    ck = os.path.join(GOLDEN, "ref_C.chunks")
+    r = subprocess.run([exe, "-z", "-b", "8", "-s", "3", "-r", "3", str(p), ck], capture_output=True, text=True, check=True)
+    assert '"chunks": 72, "ok": 72, "failed": 0' in r.stdout

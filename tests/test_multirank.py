@@ -1,0 +1,88 @@
+"""CPU, world_size 2 (gloo): the multi-GPU split and the host-side digest
+gather produce exactly the single-process digests in global chunk order.
+The per-rank hashing here is the oracle standing in for the kernel (no GPU
+in this container); the partition / gather code is the product's (shard.py,
+the same logic bench.py and bt_sha1_chunks_host_multi use)."""
+import importlib.util
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import PKG, REPO, read_pairs
+
+CHUNK = 4096  # small chunks keep the CPU oracle fast
+
+
+def _load_shard():
+    spec = importlib.util.spec_from_file_location("shard", os.path.join(PKG, "shard.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mode, q):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import py_oracle
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shard = _load_shard()
+    if mode == "weak":
+        lo, hi = shard.weak_range(rank, 5)
+        data = py_oracle.fill_synthetic((hi - lo) * CHUNK, lo * (CHUNK // 8), py_oracle.SEED_SYNTH)
+        local = b"".join(py_oracle.hash_chunks(data, CHUNK))
+    else:  # strong split of one 37-chunk image with a short tail
+        n_bytes = 36 * CHUNK + 1234
+        n = (n_bytes + CHUNK - 1) // CHUNK
+        lo, hi = shard.block_range(n, world, rank)
+        img = py_oracle.fill_synthetic(n_bytes, 0, 77)
+        local = b"".join(py_oracle.hash_chunks(bytes(img[lo * CHUNK:min(hi * CHUNK, n_bytes)]), CHUNK))
+    out = shard.gather_digests(local, world, rank)
+    if rank == 0:
+        q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["weak", "strong"])
+def test_two_rank_split_equals_single(mode, oracle):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if mode == "weak":
+        data = oracle.fill_synthetic(10 * CHUNK, 0, oracle.SEED_SYNTH)
+        want = b"".join(oracle.hash_chunks(data, CHUNK))
+    else:
+        img = oracle.fill_synthetic(36 * CHUNK + 1234, 0, 77)
+        want = b"".join(oracle.hash_chunks(bytes(img), CHUNK))
+    assert got == want
+
+
+def test_block_range_covers_exactly():
+    shard = _load_shard()
+    for n in [0, 1, 7, 8, 131072, 1048576]:
+        for world in [1, 2, 4, 8]:
+            rs = [shard.block_range(n, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+    # weak scaling at 8 GPUs = BASELINE config 4's 1 M chunks
+    assert shard.weak_range(7, 131072) == (917504, 1048576)

@@ -43,6 +43,30 @@ for step in "$@"; do
         -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline
       run pmc_valu 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc" -o valu \
         -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ;;
+    ubench) run ubench_valu 300 "$ROOT/tools/ubench/valu_rate" ;;
+    ubench_alu) run ubench_alu 300 "$ROOT/tools/ubench/sha1_alu" ;;
+    variants)
+      for v in "2 1 0" "3 1 0" "4 1 0" "2 2 0" "2 1 1" "3 1 1" "2 2 1"; do
+        set -- $v
+        run "var_$1$2$3" 300 python3 bench.py --ring $1 --lines $2 --nt $3 --steps 5 --no-cpu-baseline
+      done ;;
+    pitches)
+      for p in 524416 524544 528384 589824; do
+        run "pitch_$p" 300 python3 bench.py --pitch $p --steps 5 --no-cpu-baseline
+      done ;;
+    occupancy)
+      run occ_262144 300 python3 bench.py --ring 2 --chunks 262144 --steps 5 --no-cpu-baseline
+      run occ_393216 300 python3 bench.py --ring 2 --chunks 393216 --steps 5 --no-cpu-baseline ;;
+    counters) run counters 120 rocprofv3 -L ;;
+    stream)
+      python3 -c "import lzma; open('/tmp/C.tar','wb').write(lzma.decompress(open('tests/golden/C.tar.xz','rb').read()))"
+      VS="$ROOT/bittorrent-with-congestion-control_amd/bin/verify-stream"
+      run stream_pageable 600 python3 tools/stream_bench.py 8
+      run vs_packet_b64 300 "$VS" -b 64 -s 2 -r 64 /tmp/C.tar tests/golden/ref_C.chunks
+      run vs_packet_b1024 300 "$VS" -b 1024 -s 2 -r 1024 /tmp/C.tar tests/golden/ref_C.chunks
+      run vs_zcopy_b1024_s2 300 "$VS" -z -b 1024 -s 2 -r 8 /tmp/C.tar tests/golden/ref_C.chunks
+      run vs_zcopy_b2048_s3 300 "$VS" -z -b 2048 -s 3 -r 6 /tmp/C.tar tests/golden/ref_C.chunks
+      run vs_zcopy_b256_s4 300 "$VS" -z -b 256 -s 4 -r 32 /tmp/C.tar tests/golden/ref_C.chunks ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -37,6 +37,20 @@ for step in "$@"; do
         -- python3 "$ROOT/bench.py" --steps 10 --no-cpu-baseline ;;
     pmc)
       mkdir -p "$OUT/pmc"
+      PB="python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+      run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o fetch -- $PB
+      run pmc_rdreq 600 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc" -o rdreq -- $PB
+      run pmc_valu 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc" -o valu -- $PB
+      run pmc_valu2 600 rocprofv3 --kernel-trace --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_BUSY_CU_CYCLES --output-format csv -d "$OUT/pmc" -o valu2 -- $PB
+      run pmc_wait 600 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc" -o wait -- $PB ;;
+    bench_rings)
+      for r in 2 3 4; do run bench_ring$r 300 python3 bench.py --ring $r --steps 10 --no-cpu-baseline; done ;;
+    prof)
+      mkdir -p "$OUT/prof"
+      run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench \
+        -- python3 "$ROOT/bench.py" --steps 10 --no-cpu-baseline ;;
+    pmc)
+      mkdir -p "$OUT/pmc"
       run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o fetch \
         -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline
       run pmc_rdreq 600 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d "$OUT/pmc" -o rdreq \
@@ -67,6 +81,10 @@ for step in "$@"; do
       run vs_zcopy_b1024_s2 300 "$VS" -z -b 1024 -s 2 -r 8 /tmp/C.tar tests/golden/ref_C.chunks
       run vs_zcopy_b2048_s3 300 "$VS" -z -b 2048 -s 3 -r 6 /tmp/C.tar tests/golden/ref_C.chunks
       run vs_zcopy_b256_s4 300 "$VS" -z -b 256 -s 4 -r 32 /tmp/C.tar tests/golden/ref_C.chunks ;;
+    stream_prof)
+      mkdir -p "$OUT/stream_prof"
+      run stream_prof 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/stream_prof" -o sb \
+        -- python3 "$ROOT/tools/stream_bench.py" 4 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Turn the rocprofv3 CSVs of a gpu_session `prof` + `pmc` run into the
+committed evidence under profiles/<round>/:
+
+  kernel_stats.csv         rocprofv3 --kernel-trace --stats summary (copied)
+  pmc_summary.json         per-dispatch counters of the hot kernel, averaged
+  summary.md               human-readable table
+  ../traffic_<round>.json  HBM bytes per launch for bench.py's roofline.traffic
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE is in KiB and on gfx950
+reports half of a wide streaming read, so bytes = FETCH_SIZE * 1024 * 2; the
+memory-side request count TCC_EA0_RDREQ_sum (128-byte requests here, with
+TCC_EA0_RDREQ_32B_sum = 0) gives the same figure independently.
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+from collections import defaultdict
+
+HOT = "k_sha1_fixed"
+
+
+def counters(path):
+    per = defaultdict(lambda: defaultdict(float))  # dispatch -> counter -> value
+    meta = {}
+    for r in csv.DictReader(open(path)):
+        if HOT not in r["Kernel_Name"]:
+            continue
+        d = r["Dispatch_Id"]
+        per[d][r["Counter_Name"]] += float(r["Counter_Value"])
+        meta[d] = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Grid_Size"], r.get("VGPR_Count"))
+    return per, meta
+
+
+def main():
+    src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+    rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
+    chunks = int(sys.argv[3]) if len(sys.argv) > 3 else 131072
+    out = os.path.join("profiles", rnd)
+    os.makedirs(out, exist_ok=True)
+    stats = os.path.join(src, "prof", "bench_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copyfile(stats, os.path.join(out, "kernel_stats.csv"))
+    agg = defaultdict(list)
+    durs = []
+    for name in ("fetch", "rdreq", "valu", "valu2", "wait"):
+        p = os.path.join(src, "pmc", f"{name}_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        per, meta = counters(p)
+        for d, cs in per.items():
+            for k, v in cs.items():
+                agg[k].append(v)
+            durs.append((meta[d][1] - meta[d][0]) * 1e-6)
+    summary = {k: statistics.mean(v) for k, v in agg.items()}
+    summary["profiled_dispatches"] = len(durs)
+    summary["profiled_kernel_ms_mean"] = statistics.mean(durs) if durs else None
+    algo = chunks * 512 * 1024
+    traffic = {}
+    if "FETCH_SIZE" in summary:
+        traffic["fetch_size_bytes_corrected"] = summary["FETCH_SIZE"] * 1024 * 2
+    if "TCC_EA0_RDREQ_sum" in summary:
+        traffic["rdreq_bytes"] = summary["TCC_EA0_RDREQ_sum"] * 128 + summary.get("TCC_EA0_RDREQ_32B_sum", 0) * 32
+    json.dump(summary, open(os.path.join(out, "pmc_summary.json"), "w"), indent=1)
+    if traffic:
+        hbm = traffic.get("fetch_size_bytes_corrected", traffic.get("rdreq_bytes"))
+        tj = {"chunks": chunks, "pitch": 512 * 1024, "hbm_bytes_per_launch": hbm,
+              "algorithmic_bytes_per_launch": algo, "ratio": hbm / algo, **traffic,
+              "method": "rocprofv3 --pmc FETCH_SIZE (x1024 KiB, x2 gfx950 half-count) and TCC_EA0_RDREQ_sum x128 B, "
+                        "separate passes, hot kernel dispatches averaged"}
+        json.dump(tj, open(os.path.join("profiles", f"traffic_{rnd}.json"), "w"), indent=1)
+    lines = [f"# Profile summary {rnd}", "", f"hot kernel `{HOT}`, {chunks} x 512 KiB chunks per launch", ""]
+    if os.path.exists(stats):
+        lines += ["## rocprofv3 --kernel-trace --stats", "", "| kernel | calls | avg ms | min ms | max ms |", "|---|---|---|---|---|"]
+        for r in csv.DictReader(open(stats)):
+            lines.append(f"| {r['Name'][:70]} | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | "
+                         f"{float(r['MinNs'])/1e6:.3f} | {float(r['MaxNs'])/1e6:.3f} |")
+        lines.append("")
+    if summary:
+        lines += ["## PMC (hot kernel, mean per dispatch)", "", "| counter | value |", "|---|---|"]
+        for k, v in sorted(summary.items()):
+            lines.append(f"| {k} | {v:.6g} |" if isinstance(v, float) else f"| {k} | {v} |")
+        lines.append("")
+    if traffic:
+        lines += [f"HBM read bytes per launch: {hbm:.4g} (algorithmic {algo:.4g}, ratio {hbm/algo:.3f})", ""]
+    open(os.path.join(out, "summary.md"), "w").write("\n".join(lines))
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()

@@ -100,8 +100,8 @@ struct PinBuf {
 struct Lane {
   hipStream_t s = nullptr;
   hipEvent_t ev = nullptr;
-  PinBuf h_in, h_dig;
-  DevBuf d_in, d_dig;
+  PinBuf h_in, h_dig;  // h_dig: the kernel stores digests straight into it
+  DevBuf d_in;
   bool busy = false;
   uint64_t first = 0, count = 0;  // chunk range in flight
 };
@@ -109,7 +109,7 @@ struct Lane {
 struct DevCtx {
   int dev = 0;
   std::mutex mu;
-  hipStream_t s = nullptr;  // drop-in calls
+  hipStream_t s = nullptr;  // drop-in calls and NULL-stream launches (= lane[0].s)
   Lane lane[2];
   DevBuf d_msg, d_state;
   PinBuf h_msg, h_state;
@@ -139,23 +139,34 @@ DevCtx *ctx_for(int dev) {
   if (!g_ctx[dev]) {
     auto c = std::make_unique<DevCtx>();
     c->dev = dev;
-    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(dev) != hipSuccess) {
       set_err("cannot initialise HIP device %d", dev);
       return nullptr;
-    }
-    for (auto &l : c->lane) {
-      if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&l.ev, hipEventDisableTiming) != hipSuccess) {
-        set_err("cannot create streams on device %d", dev);
-        return nullptr;
-      }
     }
     g_ctx[dev] = std::move(c);
   }
   return g_ctx[dev].get();
 }
 
-hipStream_t pick_stream(void *stream, DevCtx *c) { return stream ? (hipStream_t)stream : c->s; }
+// Streams are created on first use and kept few: HIP multiplexes streams onto
+// GPU_MAX_HW_QUEUES (4) hardware queues, and two streams that share a queue
+// serialise -- which silently kills the H2D/hash overlap of the pipelines.
+int ensure_streams(DevCtx *c) {
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  if (c->s) return 0;
+  for (auto &l : c->lane) {
+    BT_CK(hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking));
+    BT_CK(hipEventCreateWithFlags(&l.ev, hipEventDisableTiming));
+  }
+  c->s = c->lane[0].s;
+  return 0;
+}
+
+hipStream_t pick_stream(void *stream, DevCtx *c) {
+  if (stream) return (hipStream_t)stream;
+  if (ensure_streams(c)) return nullptr;
+  return c->s;
+}
 
 bool fast_layout(const void *d_in, uint64_t chunk_len, uint64_t pitch, const void *d_dig) {
   return ((uintptr_t)d_in & 15) == 0 && (pitch & 15) == 0 && ((uintptr_t)d_dig & 3) == 0 &&
@@ -219,11 +230,11 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
     set_err("chunk_len must be in [1, 4 GiB)");
     return -1;
   }
+  if (ensure_streams(c)) return -1;
   const uint64_t bytes_per = batch_bytes_for(chunk_len, size_hint);
   const uint64_t per = bytes_per / chunk_len;
   for (auto &l : c->lane) {
-    if ((staged && l.h_in.ensure(bytes_per)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per) ||
-        l.d_dig.ensure(20 * per))
+    if ((staged && l.h_in.ensure(bytes_per)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per))
       return -1;
     l.busy = false;
   }
@@ -245,8 +256,10 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
     if (got == 0) break;
     const uint64_t cnt = ((uint64_t)got + chunk_len - 1) / chunk_len;
     BT_CK(hipMemcpyAsync(l.d_in.p, src, (size_t)got, hipMemcpyHostToDevice, l.s));
-    if (launch_image(l.d_in.as<uint8_t>(), (uint64_t)got, chunk_len, l.d_dig.as<uint8_t>(), l.s)) return -1;
-    BT_CK(hipMemcpyAsync(l.h_dig.p, l.d_dig.p, 20 * cnt, hipMemcpyDeviceToHost, l.s));
+    // Digests go straight to pinned host memory from the kernel: a D2H copy
+    // here would sit in the shared copy-engine queue behind this batch's
+    // kernel and hold up the next batch's H2D (measured: full serialisation).
+    if (launch_image(l.d_in.as<uint8_t>(), (uint64_t)got, chunk_len, l.h_dig.as<uint8_t>(), l.s)) return -1;
     BT_CK(hipEventRecord(l.ev, l.s));
     l.busy = true;
     l.first = next;
@@ -319,6 +332,7 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
 
 // Single message on the GPU (shahash): stage, ragged kernel, 20 bytes back.
 int hash_one(DevCtx *c, const uint8_t *buf, uint32_t len, uint8_t out[20]) {
+  if (ensure_streams(c)) return -1;
   if (c->h_msg.ensure((size_t)len + 64) || c->d_msg.ensure((size_t)len + 64) || c->d_state.ensure(64) ||
       c->h_state.ensure(64))
     return -1;
@@ -334,6 +348,7 @@ int hash_one(DevCtx *c, const uint8_t *buf, uint32_t len, uint8_t out[20]) {
 // Advance sc->hash over nblocks whole blocks at host address `blocks`.
 int midstate(DevCtx *c, uint32_t h[5], const uint8_t *blocks, uint64_t nblocks) {
   if (!nblocks) return 0;
+  if (ensure_streams(c)) return -1;
   const size_t bytes = (size_t)nblocks * 64;
   if (c->h_msg.ensure(bytes) || c->d_msg.ensure(bytes) || c->d_state.ensure(64) || c->h_state.ensure(64)) return -1;
   memcpy(c->h_msg.p, blocks, bytes);
@@ -412,7 +427,9 @@ int bt_sha1_chunks_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_
   BT_CK(hipGetDevice(&dev));
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
-  return launch_chunks(d_in, n, chunk_len, pitch, d_digests, pick_stream(stream, c));
+  hipStream_t st = pick_stream(stream, c);
+  if (!st) return -1;
+  return launch_chunks(d_in, n, chunk_len, pitch, d_digests, st);
 }
 
 int bt_sha1_verify_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_t pitch, const uint8_t *d_expected,
@@ -430,8 +447,10 @@ int bt_sha1_verify_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_
   BT_CK(hipGetDevice(&dev));
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
-  BT_CK(btsha1_launch_fixed(d_in, n, (uint32_t)pitch, (uint32_t)chunk_len, d_digests, d_expected, d_ok,
-                            pick_stream(stream, c), g_variant.load()));
+  hipStream_t st = pick_stream(stream, c);
+  if (!st) return -1;
+  BT_CK(btsha1_launch_fixed(d_in, n, (uint32_t)pitch, (uint32_t)chunk_len, d_digests, d_expected, d_ok, st,
+                            g_variant.load()));
   return 0;
 }
 
@@ -446,7 +465,9 @@ int bt_sha1_ragged_dev(const void *d_base, const uint64_t *d_offsets, const uint
   BT_CK(hipGetDevice(&dev));
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
-  BT_CK(btsha1_launch_ragged(d_base, d_offsets, d_lens, 0, 0, n, d_digests, pick_stream(stream, c)));
+  hipStream_t st = pick_stream(stream, c);
+  if (!st) return -1;
+  BT_CK(btsha1_launch_ragged(d_base, d_offsets, d_lens, 0, 0, n, d_digests, st));
   return 0;
 }
 
@@ -459,7 +480,9 @@ int bt_sha1_fill_synthetic(void *d_buf, uint64_t nbytes, uint64_t first_word, ui
   BT_CK(hipGetDevice(&dev));
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
-  BT_CK(btsha1_launch_fill(d_buf, nbytes, first_word, seed, pick_stream(stream, c)));
+  hipStream_t st = pick_stream(stream, c);
+  if (!st) return -1;
+  BT_CK(btsha1_launch_fill(d_buf, nbytes, first_word, seed, st));
   return 0;
 }
 
@@ -688,7 +711,7 @@ struct VBatch {
   hipStream_t s = nullptr;
   hipEvent_t ev = nullptr;
   uint8_t *h_in = nullptr, *h_exp = nullptr, *h_ok = nullptr, *h_dig = nullptr;
-  uint8_t *d_in = nullptr, *d_exp = nullptr, *d_ok = nullptr, *d_dig = nullptr;
+  uint8_t *d_in = nullptr;
   std::vector<uint64_t> tags;
   uint32_t count = 0;
   bool inflight = false;
@@ -726,11 +749,10 @@ int v_launch(bt_sha1_verifier *v) {
   if (b.count == 0) return 0;
   const size_t bytes = (size_t)b.count * v->chunk_len;
   BT_CK(hipMemcpyAsync(b.d_in, b.h_in, bytes, hipMemcpyHostToDevice, b.s));
-  BT_CK(hipMemcpyAsync(b.d_exp, b.h_exp, 20 * (size_t)b.count, hipMemcpyHostToDevice, b.s));
-  BT_CK(btsha1_launch_fixed(b.d_in, b.count, v->chunk_len, v->chunk_len, b.d_dig, b.d_exp, b.d_ok, b.s,
+  // Expected hashes are read, verdicts and digests written, by the kernel in
+  // pinned host memory: the chunk bytes are the only copy (see run_pipeline).
+  BT_CK(btsha1_launch_fixed(b.d_in, b.count, v->chunk_len, v->chunk_len, b.h_dig, b.h_exp, b.h_ok, b.s,
                             g_variant.load()));
-  BT_CK(hipMemcpyAsync(b.h_ok, b.d_ok, b.count, hipMemcpyDeviceToHost, b.s));
-  BT_CK(hipMemcpyAsync(b.h_dig, b.d_dig, 20 * (size_t)b.count, hipMemcpyDeviceToHost, b.s));
   BT_CK(hipEventRecord(b.ev, b.s));
   b.inflight = true;
   v->order.push_back(v->fill);
@@ -766,8 +788,7 @@ bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32
         hipHostMalloc((void **)&b.h_exp, 20 * (size_t)batch, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&b.h_ok, batch, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&b.h_dig, 20 * (size_t)batch, hipHostMallocDefault) != hipSuccess ||
-        hipMalloc((void **)&b.d_in, bytes) != hipSuccess || hipMalloc((void **)&b.d_exp, 20 * (size_t)batch) != hipSuccess ||
-        hipMalloc((void **)&b.d_ok, batch) != hipSuccess || hipMalloc((void **)&b.d_dig, 20 * (size_t)batch) != hipSuccess) {
+        hipMalloc((void **)&b.d_in, bytes) != hipSuccess) {
       set_err("verifier: allocation failed");
       bt_sha1_verifier_destroy(v);
       return nullptr;
@@ -788,9 +809,6 @@ void bt_sha1_verifier_destroy(bt_sha1_verifier *v) {
     if (b.h_ok) (void)hipHostFree(b.h_ok);
     if (b.h_dig) (void)hipHostFree(b.h_dig);
     if (b.d_in) (void)hipFree(b.d_in);
-    if (b.d_exp) (void)hipFree(b.d_exp);
-    if (b.d_ok) (void)hipFree(b.d_ok);
-    if (b.d_dig) (void)hipFree(b.d_dig);
   }
   delete v;
 }

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
     const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t chunk0 = (uint64_t)blockIdx.x * kBlock + (uint64_t)wave * 64u;  // wave-uniform
+  const uint64_t chunk0 = (uint64_t)blockIdx.x * blockDim.x + (uint64_t)wave * 64u;  // wave-uniform
   if (chunk0 >= n_chunks) return;
   const uint64_t left = n_chunks - chunk0;
   const uint32_t nvalid = left < 64 ? (uint32_t)left : 64u;
@@ -253,12 +253,17 @@ using namespace btsha1;
 template <int NBUF, int L, int AUX>
 static hipError_t launch_fixed_v(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
                                  const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s) {
-  const uint64_t grid = (n + kBlock - 1) / kBlock;
+  // Below one wave per SIMD (256 CUs x 4 SIMDs x 64 lanes) use one-wave
+  // workgroups so the dispatcher spreads the waves over distinct CUs instead
+  // of stacking four per CU: a chunk's latency is its serial 8193-block chain,
+  // so a lone wave per SIMD finishes the batch soonest.
+  const uint32_t wg = n < 65536 ? 64u : (uint32_t)kBlock;
+  const uint64_t grid = (n + wg - 1) / wg;
   if (d_ok)
-    hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, true>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, true>), dim3((uint32_t)grid), dim3(wg), 0, s,
                        (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok);
   else
-    hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, false>), dim3((uint32_t)grid), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, false>), dim3((uint32_t)grid), dim3(wg), 0, s,
                        (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok);
   return hipGetLastError();
 }

@@ -59,6 +59,11 @@ for step in "$@"; do
         -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ;;
     ubench) run ubench_valu 300 "$ROOT/tools/ubench/valu_rate" ;;
     ubench_alu) run ubench_alu 300 "$ROOT/tools/ubench/sha1_alu" ;;
+    mixpattern) run mixpattern 300 "$ROOT/tools/ubench/mixpattern" ;;
+    coissue)
+      run coissue 300 "$ROOT/tools/ubench/coissue"
+      mkdir -p "$OUT/coissue_pmc"
+      run coissue_pmc 300 rocprofv3 --kernel-trace --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/coissue_pmc" -o co -- "$ROOT/tools/ubench/coissue" ;;
     variants)
       for v in "2 1 0" "3 1 0" "4 1 0" "2 2 0" "2 1 1" "3 1 1" "2 2 1"; do
         set -- $v

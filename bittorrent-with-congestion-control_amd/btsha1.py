@@ -65,7 +65,8 @@ _sig("bt_sha1_chunks_file", _i64, _vp, _u64, _vp, _u64)
 _sig("bt_sha1_verifier_create", _vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32)
 _sig("bt_sha1_verifier_destroy", None, _vp)
 _sig("bt_sha1_verifier_slot", _vp, _vp)
-_sig("bt_sha1_verifier_commit", ctypes.c_int, _vp, ctypes.c_uint32, _vp, _u64)
+_sig("bt_sha1_verifier_commit", ctypes.c_int, _vp, _vp, ctypes.c_uint32, _vp, _u64)
+_sig("bt_sha1_verifier_release", ctypes.c_int, _vp, _vp)
 _sig("bt_sha1_verifier_submit", ctypes.c_int, _vp, _vp, ctypes.c_uint32, _vp, _u64)
 _sig("bt_sha1_verifier_flush", ctypes.c_int, _vp)
 _sig("bt_sha1_verifier_poll", ctypes.c_int, _vp, ctypes.POINTER(Verdict), ctypes.c_int)
@@ -240,14 +241,29 @@ class Verifier:
         e = (ctypes.c_uint8 * 20).from_buffer_copy(bytes(expected))
         _check(lib.bt_sha1_verifier_submit(self.h, buf, n, e, tag), "bt_sha1_verifier_submit")
 
-    def slot_fill(self, chunk, expected, tag):
-        """Zero-copy form: write into the pinned slot, then commit."""
+    def slot(self):
+        """Hand out a pinned slot (integer address) to assemble a chunk in."""
         p = lib.bt_sha1_verifier_slot(self.h)
         if not p:
             raise BtSha1Error(f"bt_sha1_verifier_slot: {last_error()}")
-        ctypes.memmove(p, bytes(chunk), len(chunk))
+        return p
+
+    def commit(self, slot, expected, tag, length=None):
         e = (ctypes.c_uint8 * 20).from_buffer_copy(bytes(expected))
-        _check(lib.bt_sha1_verifier_commit(self.h, len(chunk), e, tag), "bt_sha1_verifier_commit")
+        _check(lib.bt_sha1_verifier_commit(self.h, slot, length or self.chunk_len, e, tag),
+               "bt_sha1_verifier_commit")
+
+    def release(self, slot):
+        _check(lib.bt_sha1_verifier_release(self.h, slot), "bt_sha1_verifier_release")
+
+    def flush(self):
+        _check(lib.bt_sha1_verifier_flush(self.h), "bt_sha1_verifier_flush")
+
+    def slot_fill(self, chunk, expected, tag):
+        """Zero-copy form: write into a pinned slot, then commit it."""
+        p = self.slot()
+        ctypes.memmove(p, bytes(chunk), len(chunk))
+        self.commit(p, expected, tag, len(chunk))
 
     def _collect(self, fn, max_n=4096):
         out = (Verdict * max_n)()

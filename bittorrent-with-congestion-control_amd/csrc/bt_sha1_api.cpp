@@ -707,24 +707,30 @@ void SHA1Final(SHA1Context *sc, uint8_t hash[SHA1_HASH_SIZE]) {
 // ===========================================================================
 // Batched asynchronous verifier (util.c:304-337 without the synchronous hash).
 // ===========================================================================
+// A ring of `nstreams` batches of `batch` pinned chunk slots.  Slots are handed
+// out in ring order and may be committed (or released) in any order -- a peer
+// assembles up to max_conn chunks at once (util.c:250-277).  A batch launches
+// (one H2D of its slots, one hot-kernel launch with the fused verify epilogue)
+// once it is closed -- every slot handed out, or flushed -- and each of its
+// handed-out slots has been committed or released.
 struct VBatch {
   hipStream_t s = nullptr;
   hipEvent_t ev = nullptr;
   uint8_t *h_in = nullptr, *h_exp = nullptr, *h_ok = nullptr, *h_dig = nullptr;
   uint8_t *d_in = nullptr;
   std::vector<uint64_t> tags;
-  uint32_t count = 0;
-  bool inflight = false;
+  std::vector<uint8_t> state;  // per slot: 0 free, 1 handed out, 2 committed, 3 released
+  uint32_t reserved = 0, settled = 0;
+  bool closed = false, inflight = false;
 };
 
 struct bt_sha1_verifier {
   int dev = 0;
   uint32_t chunk_len = 0, batch = 0;
   std::vector<VBatch> b;
-  uint32_t fill = 0;             // batch being filled
+  uint32_t fill = 0;             // batch handing out slots
   std::deque<uint32_t> order;    // batches in flight, oldest first
   std::deque<bt_sha1_verdict> done;
-  bool slot_out = false;
   int64_t queued = 0;            // committed, verdict not yet returned
 };
 
@@ -732,32 +738,78 @@ namespace {
 
 int v_harvest(bt_sha1_verifier *v, VBatch &b) {
   BT_CK(hipEventSynchronize(b.ev));
-  for (uint32_t i = 0; i < b.count; ++i) {
+  for (uint32_t i = 0; i < b.reserved; ++i) {
+    if (b.state[i] != 2) continue;  // released slots produce no verdict
     bt_sha1_verdict r;
     r.tag = b.tags[i];
     r.ok = b.h_ok[i] ? 1 : 0;
     memcpy(r.digest, b.h_dig + 20 * i, 20);
     v->done.push_back(r);
   }
-  b.count = 0;
-  b.inflight = false;
+  std::fill(b.state.begin(), b.state.end(), 0);
+  b.reserved = b.settled = 0;
+  b.closed = b.inflight = false;
   return 0;
 }
 
-int v_launch(bt_sha1_verifier *v) {
-  VBatch &b = v->b[v->fill];
-  if (b.count == 0) return 0;
-  const size_t bytes = (size_t)b.count * v->chunk_len;
+int v_launch(bt_sha1_verifier *v, uint32_t idx) {
+  VBatch &b = v->b[idx];
+  if (b.reserved == 0) {  // closed while empty: nothing to do
+    b.closed = false;
+    return 0;
+  }
+  const size_t bytes = (size_t)b.reserved * v->chunk_len;
   BT_CK(hipMemcpyAsync(b.d_in, b.h_in, bytes, hipMemcpyHostToDevice, b.s));
   // Expected hashes are read, verdicts and digests written, by the kernel in
   // pinned host memory: the chunk bytes are the only copy (see run_pipeline).
-  BT_CK(btsha1_launch_fixed(b.d_in, b.count, v->chunk_len, v->chunk_len, b.h_dig, b.h_exp, b.h_ok, b.s,
+  BT_CK(btsha1_launch_fixed(b.d_in, b.reserved, v->chunk_len, v->chunk_len, b.h_dig, b.h_exp, b.h_ok, b.s,
                             g_variant.load()));
   BT_CK(hipEventRecord(b.ev, b.s));
   b.inflight = true;
-  v->order.push_back(v->fill);
-  v->fill = (v->fill + 1) % (uint32_t)v->b.size();
+  v->order.push_back(idx);
   return 0;
+}
+
+int v_maybe_launch(bt_sha1_verifier *v, uint32_t idx) {
+  VBatch &b = v->b[idx];
+  if (b.closed && !b.inflight && b.settled == b.reserved) return v_launch(v, idx);
+  return 0;
+}
+
+// The filling batch is closed: move the fill pointer on, waiting for the next
+// batch of the ring if it is still in flight.
+int v_advance(bt_sha1_verifier *v) {
+  const uint32_t nxt = (v->fill + 1) % (uint32_t)v->b.size();
+  VBatch &n = v->b[nxt];
+  if (n.inflight) {  // ring wrapped: harvest up to and including it
+    while (!v->order.empty()) {
+      const uint32_t o = v->order.front();
+      v->order.pop_front();
+      if (v_harvest(v, v->b[o])) return -1;
+      if (o == nxt) break;
+    }
+  } else if (n.closed) {
+    set_err("verifier: every batch holds slots that were handed out but never committed");
+    return -1;
+  }
+  v->fill = nxt;
+  return 0;
+}
+
+// Slot pointer -> (batch, index); -1 if it is not a handed-out slot.
+int v_locate(bt_sha1_verifier *v, const uint8_t *slot, uint32_t *bi, uint32_t *si) {
+  for (uint32_t k = 0; k < v->b.size(); ++k) {
+    VBatch &b = v->b[k];
+    if (slot >= b.h_in && slot < b.h_in + (size_t)v->batch * v->chunk_len) {
+      const size_t off = (size_t)(slot - b.h_in);
+      if (off % v->chunk_len || b.state[off / v->chunk_len] != 1) break;
+      *bi = k;
+      *si = (uint32_t)(off / v->chunk_len);
+      return 0;
+    }
+  }
+  set_err("verifier: pointer is not an outstanding slot");
+  return -1;
 }
 
 }  // namespace
@@ -782,6 +834,7 @@ bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32
   const size_t bytes = (size_t)batch * chunk_len;
   for (auto &b : v->b) {
     b.tags.resize(batch);
+    b.state.assign(batch, 0);
     if (hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void **)&b.h_in, bytes, hipHostMallocDefault) != hipSuccess ||
@@ -816,22 +869,18 @@ void bt_sha1_verifier_destroy(bt_sha1_verifier *v) {
 uint8_t *bt_sha1_verifier_slot(bt_sha1_verifier *v) {
   if (!v) return nullptr;
   if (hipSetDevice(v->dev) != hipSuccess) return nullptr;
+  if (v->b[v->fill].closed && v_advance(v)) return nullptr;
   VBatch &b = v->b[v->fill];
-  if (b.inflight) {  // ring wrapped: wait for this batch, keep its verdicts
-    while (!v->order.empty()) {
-      uint32_t o = v->order.front();
-      v->order.pop_front();
-      if (v_harvest(v, v->b[o])) return nullptr;
-      if (o == v->fill) break;
-    }
-  }
-  v->slot_out = true;
-  return b.h_in + (size_t)b.count * v->chunk_len;
+  const uint32_t j = b.reserved++;
+  b.state[j] = 1;
+  if (b.reserved == v->batch) b.closed = true;  // launches when its last slot settles
+  return b.h_in + (size_t)j * v->chunk_len;
 }
 
-int bt_sha1_verifier_commit(bt_sha1_verifier *v, uint32_t len, const uint8_t expected[20], uint64_t tag) {
-  if (!v || !v->slot_out || !expected) {
-    set_err("verifier_commit without a slot");
+int bt_sha1_verifier_commit(bt_sha1_verifier *v, uint8_t *slot, uint32_t len, const uint8_t expected[20],
+                            uint64_t tag) {
+  if (!v || !slot || !expected) {
+    set_err("null pointer");
     return -1;
   }
   if (len != v->chunk_len) {
@@ -839,14 +888,30 @@ int bt_sha1_verifier_commit(bt_sha1_verifier *v, uint32_t len, const uint8_t exp
     return -1;
   }
   if (hipSetDevice(v->dev) != hipSuccess) return -1;
-  VBatch &b = v->b[v->fill];
-  memcpy(b.h_exp + 20 * (size_t)b.count, expected, 20);
-  b.tags[b.count] = tag;
-  ++b.count;
+  uint32_t bi, si;
+  if (v_locate(v, slot, &bi, &si)) return -1;
+  VBatch &b = v->b[bi];
+  memcpy(b.h_exp + 20 * (size_t)si, expected, 20);
+  b.tags[si] = tag;
+  b.state[si] = 2;
+  ++b.settled;
   ++v->queued;
-  v->slot_out = false;
-  if (b.count == v->batch) return v_launch(v);
-  return 0;
+  return v_maybe_launch(v, bi);
+}
+
+int bt_sha1_verifier_release(bt_sha1_verifier *v, uint8_t *slot) {
+  if (!v || !slot) {
+    set_err("null pointer");
+    return -1;
+  }
+  if (hipSetDevice(v->dev) != hipSuccess) return -1;
+  uint32_t bi, si;
+  if (v_locate(v, slot, &bi, &si)) return -1;
+  VBatch &b = v->b[bi];
+  memset(b.h_exp + 20 * (size_t)si, 0, 20);
+  b.state[si] = 3;
+  ++b.settled;
+  return v_maybe_launch(v, bi);
 }
 
 int bt_sha1_verifier_submit(bt_sha1_verifier *v, const void *h_chunk, uint32_t len, const uint8_t expected[20],
@@ -862,17 +927,16 @@ int bt_sha1_verifier_submit(bt_sha1_verifier *v, const void *h_chunk, uint32_t l
   uint8_t *slot = bt_sha1_verifier_slot(v);
   if (!slot) return -1;
   memcpy(slot, h_chunk, len);
-  return bt_sha1_verifier_commit(v, len, expected, tag);
+  return bt_sha1_verifier_commit(v, slot, len, expected, tag);
 }
 
 int bt_sha1_verifier_flush(bt_sha1_verifier *v) {
   if (!v) return -1;
   if (hipSetDevice(v->dev) != hipSuccess) return -1;
-  if (v->slot_out) {
-    set_err("verifier_flush with an uncommitted slot");
-    return -1;
-  }
-  return v_launch(v);
+  VBatch &b = v->b[v->fill];
+  if (b.reserved == 0 || b.closed) return 0;
+  b.closed = true;
+  return v_maybe_launch(v, v->fill);
 }
 
 static int v_take(bt_sha1_verifier *v, bt_sha1_verdict *out, int max) {
@@ -906,7 +970,7 @@ int bt_sha1_verifier_drain(bt_sha1_verifier *v, bt_sha1_verdict *out, int max) {
   if (!v) return -1;
   if (bt_sha1_verifier_flush(v)) return -1;
   while (!v->order.empty()) {
-    uint32_t o = v->order.front();
+    const uint32_t o = v->order.front();
     v->order.pop_front();
     if (v_harvest(v, v->b[o])) return -1;
   }

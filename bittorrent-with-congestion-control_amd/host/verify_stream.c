@@ -128,7 +128,7 @@ int main(int argc, char **argv) {
         }
         if (corrupt && k % 7 == 3) slot[k % BT_CHUNK_SIZE] ^= 0x5a;
       }
-      if (bt_sha1_verifier_commit(v, BT_CHUNK_SIZE, exp + 20 * k, (uint64_t)k)) {
+      if (bt_sha1_verifier_commit(v, slot, BT_CHUNK_SIZE, exp + 20 * k, (uint64_t)k)) {
         fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
         return 255;
       }

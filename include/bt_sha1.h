@@ -102,16 +102,20 @@ typedef struct {
 bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32_t batch,
                                           uint32_t nstreams);
 void bt_sha1_verifier_destroy(bt_sha1_verifier *v);
-/* Zero-copy: a pinned chunk_len-byte slot the caller assembles a chunk in
- * (e.g. save_data_packet's memcpy target, util.c:275).  Blocks only if every
- * slot is in flight.  NULL on error. */
+/* Zero-copy: hand out a pinned chunk_len-byte slot to assemble one chunk in
+ * (e.g. save_data_packet's memcpy target, util.c:275).  Several slots may be
+ * outstanding (one per in-progress download); blocks only when the ring must
+ * wrap onto a batch still in flight.  NULL on error. */
 uint8_t *bt_sha1_verifier_slot(bt_sha1_verifier *v);
-/* Queue the slot last returned by bt_sha1_verifier_slot (len bytes used). */
-int bt_sha1_verifier_commit(bt_sha1_verifier *v, uint32_t len, const uint8_t expected[20], uint64_t tag);
+/* Queue an outstanding slot for verification against expected[20]. */
+int bt_sha1_verifier_commit(bt_sha1_verifier *v, uint8_t *slot, uint32_t len,
+                            const uint8_t expected[20], uint64_t tag);
+/* Give an outstanding slot back unverified (aborted download); no verdict. */
+int bt_sha1_verifier_release(bt_sha1_verifier *v, uint8_t *slot);
 /* Copying form: slot + memcpy + commit. */
 int bt_sha1_verifier_submit(bt_sha1_verifier *v, const void *h_chunk, uint32_t len,
                             const uint8_t expected[20], uint64_t tag);
-/* Launch the partially filled batch now. */
+/* Close the batch being filled; it launches once its outstanding slots are settled. */
 int bt_sha1_verifier_flush(bt_sha1_verifier *v);
 /* Non-blocking: copy up to max finished verdicts out; returns the count. */
 int bt_sha1_verifier_poll(bt_sha1_verifier *v, bt_sha1_verdict *out, int max);

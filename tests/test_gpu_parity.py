@@ -324,3 +324,34 @@ def test_verify_stream_zero_copy_mode(tmp_path):
     ck = os.path.join(GOLDEN, "ref_C.chunks")
     r = subprocess.run([exe, "-z", "-b", "8", "-s", "3", "-r", "3", str(p), ck], capture_output=True, text=True, check=True)
     assert '"chunks": 72, "ok": 72, "failed": 0' in r.stdout
+
+
+def test_verifier_concurrent_downloads_out_of_order(bt):
+    """A peer assembles up to max_conn chunks at once (util.c:250-277); slots
+    are committed in completion order, some downloads abort (released)."""
+    import ctypes
+    rng = random.Random(5)
+    img = c_tar_bytes()
+    chunks = [img[i * CHUNK:(i + 1) * CHUNK] for i in range(4)]
+    ref = [bytes.fromhex(l.split()[1]) for l in open(os.path.join(GOLDEN, "ref_C.chunks")).read().splitlines()[2:]]
+    v = bt.Verifier(batch=3, nstreams=3)
+    active, want, got = [], {}, []
+    for k in range(40):
+        p = v.slot()
+        ctypes.memmove(p, chunks[k % 4], CHUNK)
+        active.append((p, k))
+        while len(active) >= 4 or (k == 39 and active):      # complete a random in-flight download
+            p2, k2 = active.pop(rng.randrange(len(active)))
+            if k2 % 9 == 4:
+                v.release(p2)                                # aborted download: no verdict
+            else:
+                exp = ref[k2 % 4] if k2 % 5 else ref[(k2 + 1) % 4]
+                v.commit(p2, exp, tag=k2)
+                want[k2] = (k2 % 5 != 0)
+            got += v.poll()
+    got += v.drain()
+    assert {t: ok for t, ok, _ in got} == want
+    assert all(d == ref[t % 4] for t, _, d in got)
+    with pytest.raises(bt.BtSha1Error):
+        v.commit(12345, ref[0], tag=0)                     # not an outstanding slot
+    v.close()

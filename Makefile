@@ -52,8 +52,22 @@ dropin:
 	@echo "reference sources absent: using prebuilt oracle/_ref/make-chunks-dropin if present"
 endif
 
+# Host-side AddressSanitizer/UBSan build of the library + native stress driver
+# (GPU code is not instrumented; GPU ASan is not available on this pool).
+ASANDIR  := build_variants/asan
+ASANFLAGS := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer
+asan: $(ASANDIR)/host_stress
+
+$(ASANDIR)/libbtsha1.so: $(CSRC)/bt_sha1_api.cpp $(PKG)/build/sha1_kernels.o include/bt_sha1.h
+	@mkdir -p $(ASANDIR)
+	$(HIPCC) $(HIPFLAGS) -g $(ASANFLAGS) -c $(CSRC)/bt_sha1_api.cpp -o $(ASANDIR)/bt_sha1_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PKG)/build/sha1_kernels.o $(ASANDIR)/bt_sha1_api.o
+
+$(ASANDIR)/host_stress: tests/native/host_stress.c $(ASANDIR)/libbtsha1.so
+	/opt/rocm/llvm/bin/clang -g -O1 -fsanitize=address,undefined -fno-omit-frame-pointer -Iinclude -o $@ $< -L$(ASANDIR) -lbtsha1 -Wl,-rpath,'$$ORIGIN'
+
 clean:
 	rm -rf $(PKG)/build $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib tools oracle dropin clean
+.PHONY: all lib tools oracle dropin asan clean

@@ -1,0 +1,100 @@
+/*
+ * oracle/oracle_selftest.c -- TEST ONLY.  Drives the oracle restatement under
+ * -fsanitize=address,undefined (oracle/Makefile target oracle_asan): the NIST
+ * KATs of sha.c:32-38, chunk.c's "dash" round trip, every split point of the
+ * byte-buffered update around block boundaries, and the pthread batch driver.
+ * Exit status 0 = all checks passed.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+  uint64_t bits;
+  uint32_t h[5];
+  uint32_t fill;
+  uint8_t blk[64];
+} or_ctx;
+void or_sha1_init(or_ctx *c);
+void or_sha1_update(or_ctx *c, const void *data, uint32_t len);
+void or_sha1_final(or_ctx *c, uint8_t out[20]);
+void or_shahash(const uint8_t *buf, int len, uint8_t out[20]);
+void or_binary2hex(const uint8_t *buf, int len, char *hex);
+void or_hex2binary(const char *hex, int len, uint8_t *buf);
+void or_fill_synthetic(uint8_t *buf, uint64_t nbytes, uint64_t first_word, uint64_t seed);
+int or_hash_chunks(const uint8_t *base, uint64_t n, uint64_t pitch, uint32_t chunk_len, uint32_t last_len,
+                   uint8_t *out, int nthreads);
+
+static int fails = 0;
+static void expect(const char *what, const uint8_t d[20], const char *hex) {
+  char h[41];
+  or_binary2hex(d, 20, h);
+  if (strcmp(h, hex)) {
+    printf("FAIL %s: %s != %s\n", what, h, hex);
+    fails++;
+  }
+}
+
+int main(void) {
+  uint8_t d[20], e[20];
+  or_shahash((const uint8_t *)"abc", 3, d);
+  expect("abc", d, "a9993e364706816aba3e25717850c26c9cd0d89d");
+  or_shahash((const uint8_t *)"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq", 56, d);
+  expect("nist448", d, "84983e441c3bd26ebaae4aa1f95129e5e54670f1");
+  or_ctx c;
+  char buf[1000];
+  memset(buf, 'a', sizeof buf);
+  or_sha1_init(&c);
+  for (int i = 0; i < 1000; i++) or_sha1_update(&c, buf, sizeof buf);
+  or_sha1_final(&c, d);
+  expect("million_a", d, "34aa973cd4c4daa4f61eeb2bdbad27316534016f");
+  or_shahash((const uint8_t *)"dash", 4, d);
+  expect("dash", d, "f3319963720d2293ed504bb1f5c1c4a879147a34");
+  char hex[41];
+  or_binary2hex(d, 20, hex);
+  or_hex2binary(hex, 40, e);
+  if (memcmp(d, e, 20)) {
+    puts("FAIL hex round trip");
+    fails++;
+  }
+
+  /* every split point of messages around block boundaries == one-shot */
+  static uint8_t msg[300];
+  or_fill_synthetic(msg, sizeof msg, 7, 9);
+  for (uint32_t n = 0; n <= sizeof msg; n += 7) {
+    or_shahash(msg, (int)n, d);
+    for (uint32_t cut = 0; cut <= n; cut += 5) {
+      or_sha1_init(&c);
+      or_sha1_update(&c, msg, cut);
+      or_sha1_update(&c, msg + cut, n - cut);
+      or_sha1_final(&c, e);
+      if (memcmp(d, e, 20)) {
+        printf("FAIL split n=%u cut=%u\n", n, cut);
+        fails++;
+      }
+    }
+  }
+
+  /* threaded batch with a short tail == serial */
+  const uint32_t L = 4096;
+  const uint64_t n = 13, total = 12 * L + 999;
+  uint8_t *img = malloc(total), *a = malloc(20 * n), *b = malloc(20 * n);
+  or_fill_synthetic(img, total, 0, 3);
+  or_hash_chunks(img, n, L, L, 999, a, 1);
+  or_hash_chunks(img, n, L, L, 999, b, 5);
+  if (memcmp(a, b, 20 * n)) {
+    puts("FAIL threaded batch");
+    fails++;
+  }
+  or_shahash(img + 12 * L, 999, d);
+  if (memcmp(d, a + 20 * 12, 20)) {
+    puts("FAIL short tail");
+    fails++;
+  }
+  free(img);
+  free(a);
+  free(b);
+  printf("%s (%d failures)\n", fails ? "FAILED" : "ok", fails);
+  return fails != 0;
+}

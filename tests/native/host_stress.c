@@ -1,0 +1,135 @@
+/*
+ * tests/native/host_stress.c -- host-side stress of libbtsha1's C runtime
+ * (verifier slot ring, host pipelines, streaming drop-in API), built with
+ * host AddressSanitizer/UBSan against an ASan build of the library
+ * (`make asan`).  GPU code is not instrumented (not available on this pool).
+ * Digests are cross-checked between independent library paths and against
+ * the C.tar fixture digests passed on the command line:
+ *   host_stress <C.tar> <4 hex digests...>
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "bt_sha1.h"
+#include "chunk.h"
+
+static int fails = 0;
+#define CHECK(c, ...)                 \
+  do {                                \
+    if (!(c)) {                       \
+      printf("FAIL: " __VA_ARGS__);   \
+      printf("\n");                   \
+      fails++;                        \
+    }                                 \
+  } while (0)
+
+static unsigned rng = 12345;
+static unsigned rnd(unsigned n) {
+  rng = rng * 1103515245u + 12345u;
+  return (rng >> 8) % n;
+}
+
+int main(int argc, char **argv) {
+  if (argc != 6) {
+    fprintf(stderr, "usage: %s C.tar h0 h1 h2 h3\n", argv[0]);
+    return 2;
+  }
+  FILE *f = fopen(argv[1], "rb");
+  if (!f) return 2;
+  uint8_t *img = malloc(4 * BT_CHUNK_SIZE);
+  if (fread(img, 1, 4 * BT_CHUNK_SIZE, f) != 4 * BT_CHUNK_SIZE) return 2;
+  uint8_t ref[4][20];
+  for (int i = 0; i < 4; i++) hex2binary(argv[2 + i], 40, ref[i]);
+
+  /* make_chunks over the FILE* (chunk.h:25) */
+  rewind(f);
+  uint8_t rows[4][20], *rp[4] = {rows[0], rows[1], rows[2], rows[3]};
+  CHECK(make_chunks(f, rp) == 4, "make_chunks count");
+  fclose(f);
+  for (int i = 0; i < 4; i++) CHECK(!memcmp(rows[i], ref[i], 20), "make_chunks digest %d", i);
+
+  /* shahash + streaming API with random splits */
+  for (int i = 0; i < 4; i++) {
+    uint8_t d[20];
+    shahash(img + (size_t)i * BT_CHUNK_SIZE, BT_CHUNK_SIZE, d);
+    CHECK(!memcmp(d, ref[i], 20), "shahash %d", i);
+    SHA1Context c;
+    SHA1Init(&c);
+    uint32_t off = 0;
+    while (off < BT_CHUNK_SIZE) {
+      uint32_t n = 1 + rnd(200000);
+      if (n > BT_CHUNK_SIZE - off) n = BT_CHUNK_SIZE - off;
+      SHA1Update(&c, img + (size_t)i * BT_CHUNK_SIZE + off, n);
+      off += n;
+    }
+    SHA1Final(&c, d);
+    CHECK(!memcmp(d, ref[i], 20), "SHA1Update splits %d", i);
+  }
+
+  /* host pipelines: odd totals, tiny chunks, many batches */
+  for (int t = 0; t < 6; t++) {
+    uint64_t total = 1 + rnd(4 * BT_CHUNK_SIZE), cl = 64 * (1 + rnd(3000)) + rnd(64);
+    uint64_t n = (total + cl - 1) / cl;
+    uint8_t *a = malloc(20 * n), *b = malloc(20 * n);
+    CHECK(bt_sha1_chunks_host(img, total, cl, a) == (int64_t)n, "chunks_host count");
+    CHECK(bt_sha1_chunks_host_multi(img, total, cl, b, 0) == (int64_t)n, "chunks_host_multi count");
+    CHECK(!memcmp(a, b, 20 * n), "host vs multi");
+    uint8_t d[20];
+    shahash(img + (n - 1) * cl, (int)(total - (n - 1) * cl), d);
+    CHECK(!memcmp(d, a + 20 * (n - 1), 20), "short tail");
+    free(a);
+    free(b);
+  }
+
+  /* verifier ring: up to 6 outstanding slots, random commit / release order */
+  bt_sha1_verifier *v = bt_sha1_verifier_create(0, BT_CHUNK_SIZE, 5, 4);
+  CHECK(v != NULL, "verifier_create: %s", bt_sha1_last_error());
+  uint8_t *slot[8];
+  int tagof[8], nact = 0, committed = 0, seen = 0, good = 0, want_good = 0;
+  bt_sha1_verdict out[64];
+  for (int k = 0; k < 200; k++) {
+    uint8_t *p = bt_sha1_verifier_slot(v);
+    CHECK(p != NULL, "slot: %s", bt_sha1_last_error());
+    if (!p) break;
+    memcpy(p, img + (size_t)(k % 4) * BT_CHUNK_SIZE, BT_CHUNK_SIZE);
+    slot[nact] = p;
+    tagof[nact++] = k;
+    while (nact > 5 || (k == 199 && nact)) {
+      int j = (int)rnd(2 < nact ? 2 : nact);
+      int kk = tagof[j];
+      if (kk % 11 == 3) {
+        CHECK(bt_sha1_verifier_release(v, slot[j]) == 0, "release");
+      } else {
+        const uint8_t *e = (kk % 7) ? ref[kk % 4] : ref[(kk + 1) % 4];
+        CHECK(bt_sha1_verifier_commit(v, slot[j], BT_CHUNK_SIZE, e, (uint64_t)kk) == 0, "commit: %s",
+              bt_sha1_last_error());
+        committed++;
+        want_good += (kk % 7) != 0;
+      }
+      slot[j] = slot[nact - 1];
+      tagof[j] = tagof[nact - 1];
+      nact--;
+    }
+    int m = bt_sha1_verifier_poll(v, out, 64);
+    for (int i = 0; i < m; i++) {
+      seen++;
+      good += out[i].ok;
+      CHECK(out[i].ok == (int)((out[i].tag % 7) != 0), "verdict tag %llu", (unsigned long long)out[i].tag);
+      CHECK(!memcmp(out[i].digest, ref[out[i].tag % 4], 20), "digest tag %llu", (unsigned long long)out[i].tag);
+    }
+  }
+  int m;
+  while ((m = bt_sha1_verifier_drain(v, out, 64)) > 0)
+    for (int i = 0; i < m; i++) {
+      seen++;
+      good += out[i].ok;
+    }
+  CHECK(seen == committed && good == want_good, "verdicts %d/%d good %d/%d", seen, committed, good, want_good);
+  CHECK(bt_sha1_verifier_pending(v) == 0, "pending");
+  CHECK(bt_sha1_verifier_commit(v, img, BT_CHUNK_SIZE, ref[0], 1) == -1, "foreign pointer accepted");
+  bt_sha1_verifier_destroy(v);
+  free(img);
+  printf("%s (%d failures)\n", fails ? "FAILED" : "ok", fails);
+  return fails != 0;
+}

@@ -6,6 +6,7 @@ Every expected value comes from the reference itself: its fixture files
 the committed inputs (tests/golden/make_golden.py).
 """
 import hashlib
+import os
 import random
 
 import numpy as np
@@ -144,3 +145,17 @@ def test_reference_library_agrees_when_built(oracle):
         out = (ctypes.c_uint8 * 20)()
         ref.shahash((ctypes.c_uint8 * max(n, 1)).from_buffer_copy(d or b"\0"), n, out)
         assert bytes(out) == oracle.sha1(d)
+
+
+def test_oracle_under_asan_ubsan(tmp_path):
+    """Host-code sanitizers on the restatement (GPU sanitizers are not available)."""
+    import subprocess
+    from conftest import REPO
+    exe = tmp_path / "oracle_asan"
+    src = [f"{REPO}/oracle/sha1_oracle.c", f"{REPO}/oracle/oracle_selftest.c"]
+    r = subprocess.run(["gcc", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                        "-fno-omit-frame-pointer", "-pthread", "-o", str(exe)] + src, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env)
+    assert r.returncode == 0 and "ok (0 failures)" in r.stdout, r.stdout + r.stderr

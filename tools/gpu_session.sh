@@ -60,6 +60,13 @@ for step in "$@"; do
     ubench) run ubench_valu 300 "$ROOT/tools/ubench/valu_rate" ;;
     ubench_alu) run ubench_alu 300 "$ROOT/tools/ubench/sha1_alu" ;;
     mixpattern) run mixpattern 300 "$ROOT/tools/ubench/mixpattern" ;;
+    libvariants)
+      for rep in 1 2; do
+        for d in "$ROOT"/build_variants/*/; do
+          n=$(basename "$d")
+          run "libvar_${n}_$rep" 300 env BT_SHA1_LIB="$d/libbtsha1.so" python3 bench.py --steps 10 --no-cpu-baseline
+        done
+      done ;;
     dist2)
       run dist2_gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29531 bench.py --gpus 2 --backend gloo --chunks 8192 --steps 5 --warmup 2 --no-cpu-baseline ;;

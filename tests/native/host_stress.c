@@ -107,8 +107,10 @@ int main(int argc, char **argv) {
         committed++;
         want_good += (kk % 7) != 0;
       }
-      slot[j] = slot[nact - 1];
-      tagof[j] = tagof[nact - 1];
+      for (int q = j; q + 1 < nact; q++) { /* keep age order: j is one of the two oldest */
+        slot[q] = slot[q + 1];
+        tagof[q] = tagof[q + 1];
+      }
       nact--;
     }
     int m = bt_sha1_verifier_poll(v, out, 64);

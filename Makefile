@@ -22,7 +22,11 @@ $(PKG)/build/bt_sha1_api.o: $(CSRC)/bt_sha1_api.cpp $(CSRC)/sha1_launch.h includ
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(PKG)/build/sha1_kernels.o $(PKG)/build/bt_sha1_api.o
+$(PKG)/build/bt_chunks.o: $(CSRC)/bt_chunks.cpp include/bt_sha1.h include/chunk.h
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(PKG)/build/sha1_kernels.o $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libbtsha1.so
 
 # Host-side callers above the C-ABI (C, like the reference).
@@ -58,10 +62,11 @@ ASANDIR  := build_variants/asan
 ASANFLAGS := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer
 asan: $(ASANDIR)/host_stress
 
-$(ASANDIR)/libbtsha1.so: $(CSRC)/bt_sha1_api.cpp $(PKG)/build/sha1_kernels.o include/bt_sha1.h
+$(ASANDIR)/libbtsha1.so: $(CSRC)/bt_sha1_api.cpp $(CSRC)/bt_chunks.cpp $(PKG)/build/sha1_kernels.o include/bt_sha1.h
 	@mkdir -p $(ASANDIR)
 	$(HIPCC) $(HIPFLAGS) -g $(ASANFLAGS) -c $(CSRC)/bt_sha1_api.cpp -o $(ASANDIR)/bt_sha1_api.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PKG)/build/sha1_kernels.o $(ASANDIR)/bt_sha1_api.o
+	$(HIPCC) $(HIPFLAGS) -g $(ASANFLAGS) -c $(CSRC)/bt_chunks.cpp -o $(ASANDIR)/bt_chunks.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PKG)/build/sha1_kernels.o $(ASANDIR)/bt_sha1_api.o $(ASANDIR)/bt_chunks.o
 
 $(ASANDIR)/host_stress: tests/native/host_stress.c $(ASANDIR)/libbtsha1.so
 	/opt/rocm/llvm/bin/clang -g -O1 -fsanitize=address,undefined -fno-omit-frame-pointer -Iinclude -o $@ $< -L$(ASANDIR) -lbtsha1 -Wl,-rpath,'$$ORIGIN'

@@ -72,6 +72,20 @@ _sig("bt_sha1_verifier_flush", ctypes.c_int, _vp)
 _sig("bt_sha1_verifier_poll", ctypes.c_int, _vp, ctypes.POINTER(Verdict), ctypes.c_int)
 _sig("bt_sha1_verifier_drain", ctypes.c_int, _vp, ctypes.POINTER(Verdict), ctypes.c_int)
 _sig("bt_sha1_verifier_pending", _i64, _vp)
+_sig("bt_sha1_lookup_dev", ctypes.c_int, _vp, _u64, _vp, _u64, _vp, _vp)
+
+
+class ChunkEntry(ctypes.Structure):
+    _fields_ = [("id", ctypes.c_int32), ("hash", ctypes.c_uint8 * 20)]
+
+
+_sig("bt_chunks_parse_list", _i64, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ChunkEntry)))
+_sig("bt_chunks_parse_master", _i64, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
+     ctypes.POINTER(ctypes.POINTER(ChunkEntry)))
+_sig("bt_chunks_free", None, ctypes.POINTER(ChunkEntry))
+_sig("bt_chunks_write", ctypes.c_int, _vp, ctypes.c_char_p, _vp, ctypes.c_int64, ctypes.c_int32)
+_sig("bt_hex2binary_checked", ctypes.c_int, ctypes.c_char_p, ctypes.c_int, _vp)
+_sig("bt_chunks_last_error", ctypes.c_char_p)
 _sig("SHA1Init", None, ctypes.POINTER(SHA1Context))
 _sig("SHA1Update", None, ctypes.POINTER(SHA1Context), _vp, ctypes.c_uint32)
 _sig("SHA1Final", None, ctypes.POINTER(SHA1Context), _vp)
@@ -122,6 +136,61 @@ def ragged_dev(d_base, d_offsets, d_lens, n, d_digests, stream=None):
 
 def fill_synthetic(d_buf, nbytes, first_word, seed, stream=None):
     _check(lib.bt_sha1_fill_synthetic(d_buf, nbytes, first_word, seed, stream), "bt_sha1_fill_synthetic")
+
+
+def lookup_dev(d_table, n_table, d_queries, n_queries, d_index, stream=None):
+    _check(lib.bt_sha1_lookup_dev(d_table, n_table, d_queries, n_queries, d_index, stream), "bt_sha1_lookup_dev")
+
+
+# ---- .chunks files (host-side parsing/formatting) ---------------------------------
+def _entries(ptr, n):
+    try:
+        return [(ptr[i].id, bytes(ptr[i].hash)) for i in range(n)]
+    finally:
+        lib.bt_chunks_free(ptr)
+
+
+def parse_chunk_list(path):
+    """[(id, digest)] of a has/get .chunks file (util.c:64-111)."""
+    p = ctypes.POINTER(ChunkEntry)()
+    n = lib.bt_chunks_parse_list(str(path).encode(), ctypes.byref(p))
+    if n < 0:
+        raise BtSha1Error(lib.bt_chunks_last_error().decode())
+    return _entries(p, n)
+
+
+def parse_master(path):
+    """(data file name, [(id, digest)]) of a master .chunks file (util.c:113-164)."""
+    p = ctypes.POINTER(ChunkEntry)()
+    name = ctypes.create_string_buffer(1024)
+    n = lib.bt_chunks_parse_master(str(path).encode(), name, 1024, ctypes.byref(p))
+    if n < 0:
+        raise BtSha1Error(lib.bt_chunks_last_error().decode())
+    return name.value.decode(), _entries(p, n)
+
+
+def write_chunks(path, digests, master_name=None, first_id=0):
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = _vp
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [_vp]
+    raw = b"".join(digests)
+    fp = libc.fopen(str(path).encode(), b"w")
+    try:
+        buf = (ctypes.c_uint8 * max(len(raw), 1)).from_buffer_copy(raw or b"\0")
+        rc = lib.bt_chunks_write(fp, master_name.encode() if master_name else None, buf, len(digests), first_id)
+    finally:
+        libc.fclose(fp)
+    if rc:
+        raise BtSha1Error(lib.bt_chunks_last_error().decode())
+
+
+def hex2binary_checked(h):
+    hb = h.encode() if isinstance(h, str) else bytes(h)
+    out = (ctypes.c_uint8 * max(len(hb) // 2, 1))()
+    if lib.bt_hex2binary_checked(hb, len(hb), out):
+        raise ValueError(f"not hex: {h!r}")
+    return bytes(out)[:len(hb) // 2]
 
 
 # ---- host ------------------------------------------------------------------------

@@ -501,6 +501,32 @@ int bt_sha1_host_unregister(void *h_ptr) {
   return 0;
 }
 
+int bt_sha1_lookup_dev(const uint8_t *d_table, uint64_t n_table, const uint8_t *d_queries, uint64_t n_queries,
+                       int64_t *d_index, void *stream) {
+  if (n_queries == 0) return 0;
+  if ((n_table && !d_table) || !d_queries || !d_index || ((uintptr_t)d_table & 3) || ((uintptr_t)d_queries & 3)) {
+    set_err("lookup needs non-null, 4-byte aligned digest arrays");
+    return -1;
+  }
+  if (n_table >= (1ull << 31)) {
+    set_err("lookup table too large");
+    return -1;
+  }
+  int dev = 0;
+  BT_CK(hipGetDevice(&dev));
+  DevCtx *c = ctx_for(dev);
+  if (!c) return -1;
+  hipStream_t st = pick_stream(stream, c);
+  if (!st) return -1;
+  uint32_t cap = 1024;
+  while (cap < 2 * n_table) cap <<= 1;  // load factor <= 1/2
+  void *slots = nullptr;
+  BT_CK(hipMallocAsync(&slots, (size_t)cap * 4, st));
+  BT_CK(btsha1_launch_lookup(d_table, n_table, d_queries, n_queries, (uint32_t *)slots, cap, d_index, st));
+  BT_CK(hipFreeAsync(slots, st));
+  return 0;
+}
+
 int64_t bt_sha1_chunks_host(const void *h_in, uint64_t total_len, uint64_t chunk_len, uint8_t *h_digests) {
   if (total_len && (!h_in || !h_digests)) {
     set_err("null pointer");

@@ -243,6 +243,64 @@ __global__ __launch_bounds__(kBlock) void k_fill_synthetic(uint8_t *__restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// Digest lookup: get_chunk_id / find_chunk (util.c:3-39) for large tables.
+// Open addressing over a power-of-two slot array of (index+1) u32 values,
+// keyed by the digest's first 8 bytes (SHA-1 output is uniform); duplicates
+// keep the smallest index, matching the reference's first-match scan.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_digest(const uint8_t *p, uint32_t (&d)[5]) {
+  const uint32_t *q = (const uint32_t *)p;  // 20-byte records are 4-byte aligned
+#pragma unroll
+  for (int k = 0; k < 5; ++k) d[k] = q[k];
+}
+
+__device__ __forceinline__ bool same_digest(const uint32_t (&a)[5], const uint32_t (&b)[5]) {
+  return ((a[0] ^ b[0]) | (a[1] ^ b[1]) | (a[2] ^ b[2]) | (a[3] ^ b[3]) | (a[4] ^ b[4])) == 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_lookup_build(const uint8_t *__restrict__ table, uint64_t n,
+                                                         uint32_t *__restrict__ slots, uint32_t mask) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint32_t key[5];
+  load_digest(table + 20 * i, key);
+  uint32_t s = key[0] & mask;
+  for (uint32_t probe = 0; probe <= mask; ++probe, s = (s + 1) & mask) {
+    const uint32_t old = atomicCAS(&slots[s], 0u, (uint32_t)(i + 1));
+    if (old == 0) return;
+    uint32_t other[5];
+    load_digest(table + 20 * (uint64_t)(old - 1), other);
+    if (same_digest(key, other)) {
+      atomicMin(&slots[s], (uint32_t)(i + 1));
+      return;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_lookup_query(const uint8_t *__restrict__ table,
+                                                         const uint32_t *__restrict__ slots, uint32_t mask,
+                                                         const uint8_t *__restrict__ queries, uint64_t m,
+                                                         int64_t *__restrict__ index) {
+  const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q >= m) return;
+  uint32_t key[5];
+  load_digest(queries + 20 * q, key);
+  uint32_t s = key[0] & mask;
+  int64_t r = -1;
+  for (uint32_t probe = 0; probe <= mask; ++probe, s = (s + 1) & mask) {
+    const uint32_t v = slots[s];
+    if (v == 0) break;
+    uint32_t other[5];
+    load_digest(table + 20 * (uint64_t)(v - 1), other);
+    if (same_digest(key, other)) {
+      r = (int64_t)v - 1;
+      break;
+    }
+  }
+  index[q] = r;
+}
+
 }  // namespace btsha1
 
 // ---------------------------------------------------------------------------
@@ -300,6 +358,17 @@ hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const
 
 hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_t nblocks, hipStream_t s) {
   hipLaunchKernelGGL(k_sha1_midstate, dim3(1), dim3(64), 0, s, d_state, (const uint8_t *)d_data, nblocks);
+  return hipGetLastError();
+}
+
+hipError_t btsha1_launch_lookup(const uint8_t *d_table, uint64_t n, const uint8_t *d_queries, uint64_t m,
+                                uint32_t *d_slots, uint32_t cap, int64_t *d_index, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(d_slots, 0, (size_t)cap * 4, s);
+  if (e != hipSuccess) return e;
+  if (n) hipLaunchKernelGGL(k_lookup_build, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, d_table, n,
+                            d_slots, cap - 1);
+  if (m) hipLaunchKernelGGL(k_lookup_query, dim3((uint32_t)((m + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, d_table,
+                            d_slots, cap - 1, d_queries, m, d_index);
   return hipGetLastError();
 }
 

@@ -19,3 +19,7 @@ hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const
 hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_t nblocks, hipStream_t s);
 // Synthetic stream words [first_word, first_word + nbytes/8) into d_buf (16-byte aligned).
 hipError_t btsha1_launch_fill(void *d_buf, uint64_t nbytes, uint64_t first_word, uint64_t seed, hipStream_t s);
+// Digest lookup: d_index[q] = smallest i with table[i] == queries[q], else -1.
+// d_slots: cap (power of two, > n) u32 scratch.
+hipError_t btsha1_launch_lookup(const uint8_t *d_table, uint64_t n, const uint8_t *d_queries, uint64_t m,
+                                uint32_t *d_slots, uint32_t cap, int64_t *d_index, hipStream_t s);

@@ -124,6 +124,36 @@ int bt_sha1_verifier_drain(bt_sha1_verifier *v, bt_sha1_verdict *out, int max);
 /* Verdicts not yet returned (in flight + finished-unpolled). */
 int64_t bt_sha1_verifier_pending(bt_sha1_verifier *v);
 
+/* ---- digest lookup (get_chunk_id / find_chunk, util.c:3-39, on the GPU) - */
+/* d_index[q] = smallest i with digest d_table[i] == d_queries[q], else -1.
+ * Builds a transient open-addressing table in HBM (stream-ordered alloc). */
+int bt_sha1_lookup_dev(const uint8_t *d_table, uint64_t n_table, const uint8_t *d_queries,
+                       uint64_t n_queries, int64_t *d_index, void *stream);
+
+/* ---- .chunks files (host-side text formats around the hash) ------------ */
+typedef struct {
+  int32_t id;                          /* chunk id as written in the file     */
+  uint8_t hash[BT_SHA1_DIGEST_SIZE];   /* binary digest                       */
+} bt_chunk_entry;
+
+/* "<id> <40 hex>" lines (has/get files; parse_has_get_chunk_file,
+ * util.c:64-111).  *out is malloc'ed (bt_chunks_free).  Returns the count or
+ * -1 (bt_chunks_last_error()).  '#' and blank lines are skipped; malformed
+ * lines are errors (the reference silently stores garbage). */
+int64_t bt_chunks_parse_list(const char *path, bt_chunk_entry **out);
+/* Master file: "File: <data file>" / "Chunks:" header then list lines
+ * (parse_total_chunk_file, util.c:113-164; peer.c:299-305). */
+int64_t bt_chunks_parse_master(const char *path, char *data_file, size_t data_file_cap,
+                               bt_chunk_entry **out);
+void bt_chunks_free(bt_chunk_entry *entries);
+/* Write n digests as make-chunks does ("%d %s\n", make_chunks.c:49-53), ids
+ * from first_id; with a master header first when master_data_file != NULL. */
+int bt_chunks_write(void *fp /* FILE* */, const char *master_data_file, const uint8_t *digests,
+                    int64_t n, int32_t first_id);
+/* hex2binary (chunk.c:66-83) that rejects non-hex input: 0 or -1. */
+int bt_hex2binary_checked(const char *hex, int len, uint8_t *buf);
+const char *bt_chunks_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -370,3 +370,49 @@ def test_host_runtime_under_asan(tmp_path):
     r = subprocess.run([os.path.join(REPO, "build_variants", "asan", "host_stress"), str(p)] + ref,
                        capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0 and "ok (0 failures)" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def _dev_bytes(torch, b):
+    t = torch.zeros(max(len(b), 4), dtype=torch.uint8, device="cuda")
+    if b:
+        t[:len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()
+    return t
+
+
+@pytest.mark.parametrize("n_table,n_query", [(0, 5), (1, 3), (4, 4), (1000, 3000), (300000, 200000)])
+def test_digest_lookup_matches_first_match_scan(bt, torch, n_table, n_query):
+    """get_chunk_id (util.c:28-39): index of the FIRST equal digest, else -1."""
+    import hashlib
+    rng = random.Random(n_table)
+    distinct = [hashlib.sha1(str(i).encode()).digest() for i in range(max(1, n_table // 2 + 1))]
+    table = [distinct[rng.randrange(len(distinct))] for _ in range(n_table)]  # with duplicates
+    absent = [hashlib.sha1(b"absent" + str(i).encode()).digest() for i in range(50)]
+    queries = [(table[rng.randrange(n_table)] if n_table and rng.random() < 0.8 else absent[rng.randrange(50)])
+               for _ in range(n_query)]
+    first = {}
+    for i, d in enumerate(table):
+        first.setdefault(d, i)
+    dt, dq = _dev_bytes(torch, b"".join(table)), _dev_bytes(torch, b"".join(queries))
+    out = torch.full((n_query,), 7, dtype=torch.int64, device="cuda")
+    bt.lookup_dev(dt.data_ptr(), n_table, dq.data_ptr(), n_query, out.data_ptr())
+    torch.cuda.synchronize()
+    assert out.cpu().tolist() == [first.get(q, -1) for q in queries]
+
+
+def test_parse_then_lookup_then_verify_c_tar(bt, torch):
+    """The peer's flow on the reference fixtures: master file -> GPU lookup of
+    the has-file hashes -> verify the C.tar chunks against the master."""
+    name, master = bt.parse_master(os.path.join(GOLDEN, "ref_C.chunks"))
+    has = bt.parse_chunk_list(os.path.join(GOLDEN, "ref_B.chunks"))
+    dt = _dev_bytes(torch, b"".join(h for _, h in master))
+    dq = _dev_bytes(torch, b"".join(h for _, h in has))
+    out = torch.zeros(len(has), dtype=torch.int64, device="cuda")
+    bt.lookup_dev(dt.data_ptr(), len(master), dq.data_ptr(), len(has), out.data_ptr())
+    torch.cuda.synchronize()
+    assert [master[i][0] for i in out.cpu().tolist()] == [2, 3]
+    img = c_tar_bytes()
+    d = to_dev(torch, img)
+    ok = torch.zeros(4, dtype=torch.uint8, device="cuda")
+    bt.verify_dev(d.data_ptr(), 4, CHUNK, CHUNK, dt.data_ptr(), ok.data_ptr())
+    torch.cuda.synchronize()
+    assert name == "C.tar" and ok.cpu().tolist() == [1, 1, 1, 1]

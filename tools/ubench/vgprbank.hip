@@ -13,6 +13,15 @@
 #define SB(op) op " v40, v41, v45, v49\n\t" op " v44, v53, v57, v61\n\t" op " v48, v41, v45, v49\n\t" op " v52, v53, v57, v61\n\t" \
                op " v56, v41, v45, v49\n\t" op " v60, v53, v57, v61\n\t"
 
+#define L64(op) op " v[40:41], v[42:43], 5, v[44:45]\n\t" op " v[46:47], v[48:49], 5, v[50:51]\n\t" op " v[52:53], v[54:55], 5, v[56:57]\n\t" \
+               op " v[58:59], v[60:61], 5, v[62:63]\n\t" op " v[40:41], v[48:49], 5, v[56:57]\n\t" op " v[46:47], v[54:55], 5, v[62:63]\n\t"
+#define SH64(op) op " v[40:41], 5, v[42:43]\n\t" op " v[44:45], 5, v[46:47]\n\t" op " v[48:49], 5, v[50:51]\n\t" \
+               op " v[52:53], 5, v[54:55]\n\t" op " v[56:57], 5, v[58:59]\n\t" op " v[60:61], 5, v[62:63]\n\t"
+#define PKMOV(op) op " v[40:41], v[42:43], v[44:45] op_sel:[1,0]\n\t" op " v[46:47], v[48:49], v[50:51] op_sel:[1,0]\n\t" op " v[52:53], v[54:55], v[56:57] op_sel:[1,0]\n\t" \
+               op " v[58:59], v[60:61], v[62:63] op_sel:[1,0]\n\t" op " v[40:41], v[48:49], v[56:57] op_sel:[1,0]\n\t" op " v[46:47], v[54:55], v[62:63] op_sel:[1,0]\n\t"
+#define MOV(op) op " v40, v41\n\t" op " v44, v45\n\t" op " v48, v49\n\t" op " v52, v53\n\t" op " v56, v57\n\t" op " v60, v61\n\t"
+#define ADDCO(op) op " v40, vcc, v41, v42\n\t" op " v44, vcc, v45, v46\n\t" op " v48, vcc, v49, v50\n\t" op " v52, vcc, v53, v54\n\t" op " v56, vcc, v57, v58\n\t" op " v60, vcc, v61, v62\n\t"
+
 template <int P>
 __global__ __launch_bounds__(256) void kern(uint32_t *out, int iters) {
   asm volatile("v_mov_b32 v41, 1\n\tv_mov_b32 v42, 2\n\tv_mov_b32 v43, 3\n\tv_mov_b32 v45, 5\n\tv_mov_b32 v46, 6\n\tv_mov_b32 v47, 7\n\t"
@@ -24,6 +33,11 @@ __global__ __launch_bounds__(256) void kern(uint32_t *out, int iters) {
     if constexpr (P == 2) asm volatile(DB("v_bitop3_b32") DB("v_bitop3_b32") DB("v_bitop3_b32") DB("v_bitop3_b32") ::: CLOB);
     if constexpr (P == 3) asm volatile(SB("v_bitop3_b32") SB("v_bitop3_b32") SB("v_bitop3_b32") SB("v_bitop3_b32") ::: CLOB);
     if constexpr (P == 4) asm volatile(DB("v_alignbit_b32") DB("v_alignbit_b32") DB("v_alignbit_b32") DB("v_alignbit_b32") ::: CLOB);
+    if constexpr (P == 6) asm volatile(L64("v_lshl_add_u64") L64("v_lshl_add_u64") L64("v_lshl_add_u64") L64("v_lshl_add_u64") ::: CLOB);
+    if constexpr (P == 7) asm volatile(SH64("v_lshlrev_b64") SH64("v_lshlrev_b64") SH64("v_lshlrev_b64") SH64("v_lshlrev_b64") ::: CLOB);
+    if constexpr (P == 8) asm volatile(PKMOV("v_pk_mov_b32") PKMOV("v_pk_mov_b32") PKMOV("v_pk_mov_b32") PKMOV("v_pk_mov_b32") ::: CLOB);
+    if constexpr (P == 9) asm volatile(MOV("v_mov_b32") MOV("v_mov_b32") MOV("v_mov_b32") MOV("v_mov_b32") ::: CLOB);
+    if constexpr (P == 10) asm volatile(ADDCO("v_add_co_u32") ADDCO("v_add_co_u32") ADDCO("v_add_co_u32") ADDCO("v_add_co_u32") ::: CLOB, "vcc");
     if constexpr (P == 5) asm volatile(SB("v_alignbit_b32") SB("v_alignbit_b32") SB("v_alignbit_b32") SB("v_alignbit_b32") ::: CLOB);
   }
   uint32_t r;
@@ -54,11 +68,12 @@ void run(const char *name, int w) {
 int main() {
   for (int w : {2, 8}) {
     run<0>("add3 distinct banks", w);
-    run<1>("add3 same bank", w);
     run<2>("bitop3 distinct banks", w);
-    run<3>("bitop3 same bank", w);
-    run<4>("alignbit distinct banks", w);
-    run<5>("alignbit same bank", w);
+    run<6>("v_lshl_add_u64", w);
+    run<7>("v_lshlrev_b64", w);
+    run<8>("v_pk_mov_b32", w);
+    run<9>("v_mov_b32", w);
+    run<10>("v_add_co_u32", w);
   }
   return 0;
 }

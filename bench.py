@@ -230,7 +230,7 @@ def main():
         cpu = cpu_baseline(host, n, all_dig, threads)
 
     line = {
-        "metric": "GiB/s SHA-1 hashed (device-resident 512KiB chunks)",
+        "metric": "GiB/s SHA-1 hashed (device-resident 512KiB chunks) at 1/2/4/8 MI355X",
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,

@@ -70,6 +70,10 @@ for step in "$@"; do
     dist2)
       run dist2_gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29531 bench.py --gpus 2 --backend gloo --chunks 8192 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pairing)
+      run pairing 300 "$ROOT/tools/ubench/pairing"
+      mkdir -p "$OUT/pairing_pmc"
+      run pairing_pmc 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pairing_pmc" -o p -- "$ROOT/tools/ubench/pairing" ;;
     vgprbank) run vgprbank 300 "$ROOT/tools/ubench/vgprbank" ;;
     coissue)
       run coissue 300 "$ROOT/tools/ubench/coissue"

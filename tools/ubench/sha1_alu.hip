@@ -49,6 +49,23 @@ __device__ __forceinline__ void rounds(uint32_t (&w)[16], uint32_t &a, uint32_t 
   }
 }
 
+// Variant 3: whole 80-word schedule first (S-op runs), then the 80 rounds.
+template <int T>
+__device__ __forceinline__ void sched_all(uint32_t (&w)[80]) {
+  if constexpr (T < 80) {
+    w[T] = rotl(__builtin_amdgcn_bitop3_b32(w[T - 3], w[T - 8], w[T - 14], 0x96) ^ w[T - 16], 1);
+    sched_all<T + 1>(w);
+  }
+}
+template <int T>
+__device__ __forceinline__ void rounds_w80(const uint32_t (&w)[80], uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d,
+                                           uint32_t &e) {
+  if constexpr (T < 80) {
+    sha1_round<T>(a, b, c, d, e, w[T]);
+    rounds_w80<T + 1>(w, a, b, c, d, e);
+  }
+}
+
 template <int V>
 __global__ __launch_bounds__(256) void kern(uint32_t *out, unsigned long long *clk, int nblocks) {
   uint32_t h[5] = {kIV0, kIV1, kIV2, kIV3, kIV4};
@@ -60,7 +77,16 @@ __global__ __launch_bounds__(256) void kern(uint32_t *out, unsigned long long *c
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = bswap(m[j] ^ blk);
     uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
-    rounds<V, 0>(w, a, b, c, d, e);
+    if constexpr (V == 3) {
+      uint32_t w80[80];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w80[j] = w[j];
+      sched_all<16>(w80);
+      __builtin_amdgcn_sched_barrier(0);
+      rounds_w80<0>(w80, a, b, c, d, e);
+    } else {
+      rounds<V, 0>(w, a, b, c, d, e);
+    }
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
   }
   unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -93,8 +119,10 @@ void run(int waves_per_simd, int ops_per_block) {
 }
 
 int main() {
-  for (int w : {1, 2, 3, 4, 8}) run<0>(w, 613);
-  for (int w : {2, 4}) run<1>(w, 613 + 160);
-  for (int w : {2, 4}) run<2>(w, 613 + 160);
+  for (int rep = 0; rep < 2; ++rep)
+    for (int w : {2, 4}) {
+      run<0>(w, 613);
+      run<3>(w, 613);
+    }
   return 0;
 }

@@ -37,6 +37,9 @@ VALU_OPS_PER_BLOCK = 613       # counted in the kernel's ISA (DESIGN.md §kernel
 
 
 def load_btsha1():
+    if not os.path.exists(os.path.join(PKG, "libbtsha1.so")):  # clean checkout
+        import subprocess
+        subprocess.run(["make", "-C", HERE, "lib"], check=True)
     spec = importlib.util.spec_from_file_location("btsha1", os.path.join(PKG, "btsha1.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)

@@ -19,6 +19,13 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+    # A clean checkout has no built artefacts (they are git-ignored): build them
+    # once (hipcc for gfx950 + gcc for the oracle), as __graft_entry__.build() does.
+    need = [os.path.join(PKG, "libbtsha1.so"), os.path.join(PKG, "bin", "make-chunks"),
+            os.path.join(REPO, "oracle", "liboracle_sha1.so")]
+    if not all(os.path.exists(p) for p in need):
+        import subprocess
+        subprocess.run(["make", "-C", REPO, "-j8", "all"], check=True)
 
 
 def load_btsha1():

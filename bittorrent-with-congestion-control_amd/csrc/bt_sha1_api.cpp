@@ -170,7 +170,7 @@ hipStream_t pick_stream(void *stream, DevCtx *c) {
 
 bool fast_layout(const void *d_in, uint64_t chunk_len, uint64_t pitch, const void *d_dig) {
   return ((uintptr_t)d_in & 15) == 0 && (pitch & 15) == 0 && ((uintptr_t)d_dig & 3) == 0 &&
-         chunk_len <= pitch && pitch <= (64ull << 20) && chunk_len < (1ull << 32);
+         chunk_len <= pitch && 64 * pitch + 4096 <= (1ull << 32);  // 32-bit buffer offsets incl. prefetch overrun
 }
 
 // Launch the right kernel(s) for n equal chunks of len bytes at pitch.

@@ -65,7 +65,8 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
   // Lanes past the end re-hash the wave's last chunk (no divergence, no store).
   const uint32_t mine = lane < nvalid ? lane : nvalid - 1u;
   const uint32_t voff = mine * pitch;
-  const uint32_t nrec = (nvalid - 1u) * pitch + ((len + 3u) & ~3u);  // bytes this wave may read
+  // Bytes this wave may read; the host guarantees 64*pitch + 4096 <= 2^32.
+  const uint32_t nrec = (nvalid - 1u) * pitch + ((len + 3u) & ~3u);
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc((void *)(base + chunk0 * (uint64_t)pitch), (short)0, (int)nrec, 0x00020000);
 

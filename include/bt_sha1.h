@@ -56,7 +56,7 @@ int bt_sha1_set_variant(int nbuf, int lines, int nt);
 /* n chunks of chunk_len bytes, chunk i at d_in + i*pitch (pitch >= chunk_len).
  * d_digests receives 20*n bytes, digest i = SHA-1(chunk i) as sha.c:545-556
  * serialises it.  Fast path when d_in and pitch are 16-byte aligned and
- * 64*pitch < 4 GiB; any other layout takes the generic kernel. */
+ * 64*pitch + 4096 <= 4 GiB; any other layout takes the generic kernel. */
 int bt_sha1_chunks_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_t pitch,
                        uint8_t *d_digests, void *stream);
 /* Same, then compares with d_expected (20*n): d_ok[i] = 1 iff equal

@@ -16,6 +16,13 @@
 #define C8 C(0) C(1) C(2) C(3) C(4) C(5) C(6) C(7)
 #define CS8 C(0) S(1) C(2) S(3) C(4) S(5) C(6) S(7)
 
+#define CSS8 C(0) S(1) S(2) C(3) S(4) S(5) C(6) S(7)
+#define CCSS8 C(0) C(1) S(2) S(3) C(4) C(5) S(6) S(7)
+#define CCS8 C(0) C(1) S(2) C(3) C(4) S(5) C(6) C(7)
+#define S1CH S(0) S(0) S(0) S(0) S(0) S(0) S(0) S(0)
+#define S2CH S(0) S(1) S(0) S(1) S(0) S(1) S(0) S(1)
+#define CB8 C(0) B(1) C(2) B(3) C(4) B(5) C(6) B(7)
+
 template <int M>
 __global__ __launch_bounds__(512) void kern(uint32_t *out, int iters) {
   uint32_t a[8];
@@ -24,12 +31,27 @@ __global__ __launch_bounds__(512) void kern(uint32_t *out, int iters) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   bool s_wave;
   if constexpr (M == 0 || M == 5) s_wave = true;
+  else if constexpr (M == 13) s_wave = w < 4;
   else if constexpr (M == 1) s_wave = false;
   else if constexpr (M == 2 || M == 6) s_wave = w < 4;
   else s_wave = (w & 1) == 0;
   for (int it = 0; it < iters; ++it) {
     if constexpr (M == 4) {
       CS8 CS8 CS8
+    } else if constexpr (M == 7) {
+      CSS8 CSS8 CSS8
+    } else if constexpr (M == 8) {
+      CCSS8 CCSS8 CCSS8
+    } else if constexpr (M == 9) {
+      CCS8 CCS8 CCS8
+    } else if constexpr (M == 10) {
+      S1CH S1CH S1CH
+    } else if constexpr (M == 11) {
+      S2CH S2CH S2CH
+    } else if constexpr (M == 12) {
+      CB8 CB8 CB8
+    } else if constexpr (M == 13) {
+      if (s_wave) { CS8 CS8 CS8 } else { S(0) CS8 CS8 CS8 }  // SIMD partner offset by one
     } else if constexpr (M == 5) {
       B8 B8 B8
     } else if constexpr (M == 6) {
@@ -71,5 +93,12 @@ int main() {
   run<4>("all alternate add3,xor");
   run<5>("all bitop3");
   run<6>("waves0-3 bitop3, 4-7 add3");
+  run<7>("all C S S");
+  run<8>("all C C S S");
+  run<9>("all C C S (SHA-1 ratio)");
+  run<10>("all xor, 1 dependent chain");
+  run<11>("all xor, 2 chains");
+  run<12>("all alternate add3,bitop3");
+  run<13>("C,S alt; waves4-7 offset 1");
   return 0;
 }

@@ -440,7 +440,7 @@ int bt_sha1_verify_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_
     return -1;
   }
   if (!fast_layout(d_in, chunk_len, pitch, d_digests)) {
-    set_err("verify needs a 16-byte aligned layout with pitch <= 64 MiB");
+    set_err("verify needs a 16-byte aligned layout with 64*pitch + 4096 <= 4 GiB");
     return -1;
   }
   int dev = 0;
@@ -843,8 +843,8 @@ int v_locate(bt_sha1_verifier *v, const uint8_t *slot, uint32_t *bi, uint32_t *s
 extern "C" {
 
 bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32_t batch, uint32_t nstreams) {
-  if (chunk_len == 0 || (chunk_len & 15) || chunk_len > (64u << 20) || batch == 0) {
-    set_err("verifier: chunk_len must be a 16-byte multiple <= 64 MiB and batch > 0");
+  if (chunk_len == 0 || (chunk_len & 15) || chunk_len > (32u << 20) || batch == 0) {
+    set_err("verifier: chunk_len must be a 16-byte multiple <= 32 MiB and batch > 0");
     return nullptr;
   }
   if (!ctx_for(device)) return nullptr;

@@ -403,7 +403,7 @@ const char *bt_sha1_build_info(void) {
 int bt_sha1_set_ring_depth(int nbuf) { return bt_sha1_set_variant(nbuf, 1, 0); }
 
 int bt_sha1_set_variant(int nbuf, int lines, int nt) {
-  const int code = nbuf == 9 ? 900 : nbuf * 100 + lines * 10 + (nt ? 1 : 0);
+  const int code = nbuf * 100 + lines * 10 + (nt ? 1 : 0);
   if (!btsha1_fixed_variant_ok(code)) {
     set_err("no hot-kernel variant ring=%d lines=%d nt=%d", nbuf, lines, nt);
     return -1;

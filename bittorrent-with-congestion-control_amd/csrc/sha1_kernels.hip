@@ -137,160 +137,6 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
 }
 
 // ---------------------------------------------------------------------------
-// Split hot kernel: a loader/schedule wave and a round wave per 64 chunks.
-//
-// At the BASELINE size (131072 chunks = 2048 waves) the one-wave-per-64-chunks
-// kernel runs at exactly 2 waves per SIMD, where the VALU issues one wave64
-// instruction per ~2 ns (tools/ubench: half-rate ops 1.95 ns at 2 waves vs
-// 1.76 at 8).  Here every workgroup has two waves for the same 64 chunks:
-//   wave S loads the message (register ring of 128-byte lines), byte-swaps,
-//          expands the schedule and adds K (sha.c:186-200 + the K of DO_ROUND),
-//          writing W+K for 40 rounds at a time into an LDS slot;
-//   wave R runs the 80 rounds of each block from LDS and owns the state.
-// Two 10 KiB slots per workgroup, one s_barrier per half block: S fills slot
-// p&1 while R consumes slot (p-1)&1.  2048 workgroups x 20 KiB LDS = 8 per CU
-// -> 4 waves per SIMD, and the rounds lose the K add (3 half-rate + 2 full-rate
-// ops per round instead of 4 + 1).  Needs len % 256 == 0 (512 KiB chunks).
-// ---------------------------------------------------------------------------
-template <int T>
-__device__ __forceinline__ constexpr uint32_t kconst() {
-  return T < 20 ? 0x5a827999u : T < 40 ? 0x6ed9eba1u : T < 60 ? 0x8f1bbcdcu : 0xca62c1d6u;  // sha.c:66-69
-}
-
-// Rounds T..T+3 from one 16-byte LDS word group of W+K.
-template <int T>
-__device__ __forceinline__ void round_wk(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
-                                         uint32_t wk) {
-  uint32_t f;
-  if constexpr (T < 20) f = f_ch(b, c, d);
-  else if constexpr (T < 40) f = f_par(b, c, d);
-  else if constexpr (T < 60) f = f_maj(b, c, d);
-  else f = f_par(b, c, d);
-  const uint32_t t = rotl(a, 5) + (f + e + wk);
-  e = d;
-  d = c;
-  c = rotl(b, 30);
-  b = a;
-  a = t;
-}
-
-template <int T, int TEND>
-__device__ __forceinline__ void consume_groups(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
-                                               const u32x4 *slot, uint32_t lane) {
-  if constexpr (T < TEND) {
-    const u32x4 q = slot[((T % 40) / 4) * 64 + lane];
-    round_wk<T>(a, b, c, d, e, q.x);
-    round_wk<T + 1>(a, b, c, d, e, q.y);
-    round_wk<T + 2>(a, b, c, d, e, q.z);
-    round_wk<T + 3>(a, b, c, d, e, q.w);
-    consume_groups<T + 4, TEND>(a, b, c, d, e, slot, lane);
-  }
-}
-
-template <int T, int TEND>
-__device__ __forceinline__ void produce_groups(uint32_t (&w)[16], u32x4 *slot, uint32_t lane) {
-  if constexpr (T < TEND) {
-    u32x4 q;
-    q.x = sched<T>(w) + kconst<T>();
-    q.y = sched<T + 1>(w) + kconst<T + 1>();
-    q.z = sched<T + 2>(w) + kconst<T + 2>();
-    q.w = sched<T + 3>(w) + kconst<T + 3>();
-    slot[((T % 40) / 4) * 64 + lane] = q;
-    produce_groups<T + 4, TEND>(w, slot, lane);
-  }
-}
-
-// One block through the S wave: two half-block phases, one barrier each.
-__device__ __forceinline__ void produce_block(uint32_t (&w)[16], u32x4 (*lds)[10 * 64], uint32_t lane) {
-  produce_groups<0, 40>(w, lds[0], lane);
-  __syncthreads();
-  produce_groups<40, 80>(w, lds[1], lane);
-  __syncthreads();
-}
-
-template <bool VERIFY>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sha1_split(
-    const uint8_t *__restrict__ base, uint64_t n_chunks, uint32_t pitch, uint32_t len, uint8_t *__restrict__ digests,
-    const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok) {
-  __shared__ u32x4 lds[2][10 * 64];  // 2 slots x 40 words x 64 lanes = 20 KiB
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t chunk0 = (uint64_t)blockIdx.x * 64u;  // grid = ceil(n/64): chunk0 < n
-  const uint64_t left = n_chunks - chunk0;
-  const uint32_t nvalid = left < 64 ? (uint32_t)left : 64u;
-  const uint32_t mine = lane < nvalid ? lane : nvalid - 1u;
-  const uint32_t nblocks = len >> 6;  // even, >= 4
-  if (wave == 0) {
-    // ---- S: loader + schedule ----------------------------------------------
-    const uint32_t voff = mine * pitch;
-    const uint32_t nrec = (nvalid - 1u) * pitch + len;
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(base + chunk0 * (uint64_t)pitch), (short)0, (int)nrec, 0x00020000);
-    u32x4 ring0[8], ring1[8];
-    load_slot<1, 0>(ring0, rsrc, voff, 0);
-    for (uint32_t line = 0; line < (nblocks >> 1); line += 2) {
-      load_slot<1, 0>(ring1, rsrc, voff, (line + 1) * 128u);  // past the end: range-checked zeros
-      __builtin_amdgcn_sched_barrier(0);
-      uint32_t w[16];
-      block_from_le(w, ring0[0], ring0[1], ring0[2], ring0[3]);
-      produce_block(w, lds, lane);
-      block_from_le(w, ring0[4], ring0[5], ring0[6], ring0[7]);
-      produce_block(w, lds, lane);
-      load_slot<1, 0>(ring0, rsrc, voff, (line + 2) * 128u);
-      __builtin_amdgcn_sched_barrier(0);
-      block_from_le(w, ring1[0], ring1[1], ring1[2], ring1[3]);
-      produce_block(w, lds, lane);
-      block_from_le(w, ring1[4], ring1[5], ring1[6], ring1[7]);
-      produce_block(w, lds, lane);
-    }
-    // MD padding block of a whole-block message (sha.c:536-543).
-    uint32_t w[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = 0u;
-    w[0] = 0x80000000u;
-    const uint64_t bits = (uint64_t)len * 8u;
-    w[14] = (uint32_t)(bits >> 32);
-    w[15] = (uint32_t)bits;
-    produce_block(w, lds, lane);
-    __syncthreads();  // pairs with R's final barrier
-  } else {
-    // ---- R: rounds --------------------------------------------------------
-    State st;
-    st.init();
-    __syncthreads();  // slot 0 of block 0 is ready
-    for (uint32_t b = 0; b <= nblocks; ++b) {
-      uint32_t a = st.h0, bb = st.h1, c = st.h2, d = st.h3, e = st.h4;
-      consume_groups<0, 40>(a, bb, c, d, e, lds[0], lane);
-      __syncthreads();
-      consume_groups<40, 80>(a, bb, c, d, e, lds[1], lane);
-      __syncthreads();
-      st.h0 += a;  // sha.c:446-450
-      st.h1 += bb;
-      st.h2 += c;
-      st.h3 += d;
-      st.h4 += e;
-    }
-    if (lane < nvalid) {
-      const uint64_t idx = chunk0 + lane;
-      const uint32_t d0 = bswap(st.h0), d1 = bswap(st.h1), d2 = bswap(st.h2), d3 = bswap(st.h3), d4 = bswap(st.h4);
-      if (digests) {
-        uint32_t *o = (uint32_t *)(digests + idx * 20u);
-        o[0] = d0; o[1] = d1; o[2] = d2; o[3] = d3; o[4] = d4;
-      }
-      if constexpr (VERIFY) {
-        const uint8_t *x = expected + idx * 20u;
-        uint32_t ex[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-          ex[k] = (uint32_t)x[4 * k] | ((uint32_t)x[4 * k + 1] << 8) | ((uint32_t)x[4 * k + 2] << 16) |
-                  ((uint32_t)x[4 * k + 3] << 24);
-        ok[idx] = (uint8_t)((ex[0] == d0) & (ex[1] == d1) & (ex[2] == d2) & (ex[3] == d3) & (ex[4] == d4));
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Generic paths (64-bit addressing, any alignment).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t load_be_word(const uint8_t *p, uint32_t align) {
@@ -486,34 +332,15 @@ static hipError_t launch_fixed_v(const void *d_in, uint64_t n, uint32_t pitch, u
   X(2, 1, 2) X(3, 1, 2) X(2, 2, 2)
 
 bool btsha1_fixed_variant_ok(int code) {
-  if (code == 900) return true;
 #define BT_CASE(N, L, A) if (code == N * 100 + L * 10 + (A ? 1 : 0)) return true;
   BT_FIXED_VARIANTS(BT_CASE)
 #undef BT_CASE
   return false;
 }
 
-static hipError_t launch_split(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
-                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s) {
-  const uint64_t grid = (n + 63) / 64;
-  if (d_ok)
-    hipLaunchKernelGGL((k_sha1_split<true>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_in, n, pitch,
-                       len, d_dig, d_exp, d_ok);
-  else
-    hipLaunchKernelGGL((k_sha1_split<false>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_in, n, pitch,
-                       len, d_dig, d_exp, d_ok);
-  return hipGetLastError();
-}
-
 hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
                                const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant) {
   if (n == 0) return hipSuccess;
-  // Split kernel (variant 900) takes whole-256-byte lengths; anything else
-  // falls back to the ring kernel.
-  if (variant == 900) {
-    if (len >= 256 && (len & 255) == 0) return launch_split(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
-    variant = 310;
-  }
 #define BT_CASE(N, L, A) \
   if (variant == N * 100 + L * 10 + (A ? 1 : 0)) return launch_fixed_v<N, L, A>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
   BT_FIXED_VARIANTS(BT_CASE)

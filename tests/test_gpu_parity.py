@@ -121,11 +121,10 @@ def synth4096(bt, torch, oracle):
     return buf
 
 
-@pytest.mark.parametrize("ring", [2, 3, 4, 9])
+@pytest.mark.parametrize("ring", [2, 3, 4])
 def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, ring):
-    """BASELINE config 2: 4096 synthetic 512 KiB chunks, every digest == sha.c's
-    (ring kernels 2/3/4 slots and the split loader/round-wave kernel, 9)."""
-    bt.set_variant(ring, 1 if ring != 9 else 0, 0)
+    """BASELINE config 2: 4096 synthetic 512 KiB chunks, every digest == sha.c's."""
+    bt.set_ring_depth(ring)
     try:
         n = 4096
         out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
@@ -138,9 +137,7 @@ def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, ring):
         bt.set_ring_depth(3)
 
 
-@pytest.mark.parametrize("ring", [3, 9])
-def test_verify_dev_flags_mismatches(bt, torch, synth4096, ring):
-    bt.set_variant(ring, 1 if ring != 9 else 0, 0)
+def test_verify_dev_flags_mismatches(bt, torch, synth4096):
     n = 1000
     golden = read_pairs("synth4096.txt")[:n]
     exp = bytearray(b"".join(bytes.fromhex(h) for _, h in golden))
@@ -156,7 +153,6 @@ def test_verify_dev_flags_mismatches(bt, torch, synth4096, ring):
     assert [i for i, v in enumerate(okl) if v == 0] == sorted(bad)
     assert all(v == 1 for i, v in enumerate(okl) if i not in bad)
     assert digests_of(torch, dig, 3)[2].hex() == golden[2][1]
-    bt.set_ring_depth(3)
 
 
 @pytest.mark.parametrize("chunk_len,pitch,n", [
@@ -178,8 +174,8 @@ def test_fixed_layouts_vs_oracle(bt, torch, oracle, chunk_len, pitch, n):
 
 
 def test_every_ring_depth_on_ragged_line_counts(bt, torch, oracle):
-    for ring in (2, 3, 4, 9):
-        bt.set_variant(ring, 1 if ring != 9 else 0, 0)
+    for ring in (2, 3, 4):
+        bt.set_ring_depth(ring)
         for blocks in range(0, 2 * 2 * ring + 3):
             for r in (0, 5, 56):
                 L = 64 * blocks + r

@@ -67,11 +67,6 @@ for step in "$@"; do
           run "libvar_${n}_$rep" 300 env BT_SHA1_LIB="$d/libbtsha1.so" python3 bench.py --steps 10 --no-cpu-baseline
         done
       done ;;
-    split)
-      for rep in 1 2; do
-        run "split_ring3_$rep" 300 python3 bench.py --ring 3 --steps 10 --no-cpu-baseline
-        run "split_ring9_$rep" 300 python3 bench.py --ring 9 --lines 0 --steps 10 --no-cpu-baseline
-      done ;;
     dist2)
       run dist2_gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29531 bench.py --gpus 2 --backend gloo --chunks 8192 --steps 5 --warmup 2 --no-cpu-baseline ;;

@@ -69,17 +69,6 @@ for step in "$@"; do
       done ;;
 <<<<<<< Updated upstream
 =======
-    split_pmc)
-      mkdir -p "$OUT/split_pmc"
-      PB="python3 $ROOT/bench.py --ring 9 --lines 0 --steps 2 --warmup 1 --no-cpu-baseline"
-      run spmc_a 600 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/split_pmc" -o a -- $PB
-      run spmc_b 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU2 SQ_WAVES --output-format csv -d "$OUT/split_pmc" -o b -- $PB ;;
-    split)
-      for rep in 1 2; do
-        run "split_ring3_$rep" 300 python3 bench.py --ring 3 --steps 10 --no-cpu-baseline
-        run "split_ring9_$rep" 300 python3 bench.py --ring 9 --lines 0 --steps 10 --no-cpu-baseline
-      done ;;
->>>>>>> Stashed changes
     dist2)
       run dist2_gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29531 bench.py --gpus 2 --backend gloo --chunks 8192 --steps 5 --warmup 2 --no-cpu-baseline ;;

@@ -43,20 +43,6 @@ for step in "$@"; do
       run pmc_valu 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc" -o valu -- $PB
       run pmc_valu2 600 rocprofv3 --kernel-trace --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_BUSY_CU_CYCLES --output-format csv -d "$OUT/pmc" -o valu2 -- $PB
       run pmc_wait 600 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc" -o wait -- $PB ;;
-    bench_rings)
-      for r in 2 3 4; do run bench_ring$r 300 python3 bench.py --ring $r --steps 10 --no-cpu-baseline; done ;;
-    prof)
-      mkdir -p "$OUT/prof"
-      run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench \
-        -- python3 "$ROOT/bench.py" --steps 10 --no-cpu-baseline ;;
-    pmc)
-      mkdir -p "$OUT/pmc"
-      run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o fetch \
-        -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline
-      run pmc_rdreq 600 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d "$OUT/pmc" -o rdreq \
-        -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline
-      run pmc_valu 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc" -o valu \
-        -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ;;
     ubench) run ubench_valu 300 "$ROOT/tools/ubench/valu_rate" ;;
     ubench_alu) run ubench_alu 300 "$ROOT/tools/ubench/sha1_alu" ;;
     mixpattern) run mixpattern 300 "$ROOT/tools/ubench/mixpattern" ;;
@@ -67,8 +53,6 @@ for step in "$@"; do
           run "libvar_${n}_$rep" 300 env BT_SHA1_LIB="$d/libbtsha1.so" python3 bench.py --steps 10 --no-cpu-baseline
         done
       done ;;
-<<<<<<< Updated upstream
-=======
     dist2)
       run dist2_gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29531 bench.py --gpus 2 --backend gloo --chunks 8192 --steps 5 --warmup 2 --no-cpu-baseline ;;

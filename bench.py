@@ -43,9 +43,13 @@ VALU_MIX_PEAK_TOPS = VALU_OPS_PER_BLOCK * 64 * SIMDS * CLOCK_GHZ * 1e9 / _MIX_CL
 
 
 def load_btsha1():
-    if not os.path.exists(os.path.join(PKG, "libbtsha1.so")):  # clean checkout
+    if not os.path.exists(os.path.join(PKG, "libbtsha1.so")):  # clean checkout: build once
+        import fcntl
         import subprocess
-        subprocess.run(["make", "-C", HERE, "lib"], check=True)
+        with open(os.path.join(HERE, ".build.lock"), "w") as lk:  # N ranks start together
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            if not os.path.exists(os.path.join(PKG, "libbtsha1.so")):
+                subprocess.run(["make", "-C", HERE, "lib"], check=True)
     spec = importlib.util.spec_from_file_location("btsha1", os.path.join(PKG, "btsha1.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)

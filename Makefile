@@ -71,8 +71,17 @@ $(ASANDIR)/libbtsha1.so: $(CSRC)/bt_sha1_api.cpp $(CSRC)/bt_chunks.cpp $(PKG)/bu
 $(ASANDIR)/host_stress: tests/native/host_stress.c $(ASANDIR)/libbtsha1.so
 	/opt/rocm/llvm/bin/clang -g -O1 -fsanitize=address,undefined -fno-omit-frame-pointer -Iinclude -o $@ $< -L$(ASANDIR) -lbtsha1 -Wl,-rpath,'$$ORIGIN'
 
+# Microbenchmarks behind the measurements in profiles/ (not part of the product).
+UB_SRC := $(wildcard tools/ubench/*.hip)
+UB_BIN := $(UB_SRC:.hip=) tools/ubench/residency
+ubench: $(UB_BIN)
+tools/ubench/%: tools/ubench/%.hip $(CSRC)/sha1_device.h
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -I$(CSRC) -o $@ $<
+tools/ubench/residency: tools/ubench/residency.cpp $(LIB)
+	$(HIPCC) -O2 -std=c++17 -I$(CSRC) -o $@ $< -L$(PKG) -lbtsha1 -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
+
 clean:
 	rm -rf $(PKG)/build $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib tools oracle dropin asan clean
+.PHONY: all lib tools oracle dropin asan ubench clean

@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/gpu_session.sh STEP... -- run GPU steps on the gpurun box, each under
 # its own time limit, stopping at the first crash/timeout/abort (never retry).
-# Steps: smoke | tests | bench | prof | pmc | scale
+# Steps: smoke | tests | bench | prof | pmc | residency | power | ... (see case below)
 # Outputs land in gpurun_out/ (merged back by gpurun).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -78,6 +78,23 @@ for step in "$@"; do
       run occ_262144 300 python3 bench.py --ring 2 --chunks 262144 --steps 5 --no-cpu-baseline
       run occ_393216 300 python3 bench.py --ring 2 --chunks 393216 --steps 5 --no-cpu-baseline ;;
     counters) run counters 120 rocprofv3 -L ;;
+    residency) run residency 300 "$ROOT/tools/ubench/residency" ;;
+    power_residency)
+      # ~20 s per mode; power/clock sampled every second alongside
+      ( for i in $(seq 1 100); do echo "T $(date +%T)"; timeout 10 amd-smi metric -g 0 -p -c 2>&1 \
+          | grep -E "SOCKET_POWER|GFX_0:" -A1; sleep 1; done ) > "$OUT/power_residency_samples.log" 2>&1 &
+      sp=$!
+      run power_residency 300 "$ROOT/tools/ubench/residency" 131072 1000 1
+      echo "T $(date +%T) alu_long start" >> "$OUT/power_residency_samples.log"
+      run power_alu_long 300 "$ROOT/tools/ubench/sha1_alu" long 3000
+      wait $sp ;;
+    power)
+      # sample board power and clocks while a ~30 s hot-kernel run is in flight
+      ( for i in $(seq 1 12); do date +%T; timeout 10 amd-smi metric -g 0 -p -c 2>&1
+          timeout 10 rocm-smi --showpower --showgpuclocks 2>&1; sleep 2; done ) > "$OUT/power_samples.log" 2>&1 &
+      sp=$!
+      run power_bench 300 python3 bench.py --steps 1500 --warmup 3 --no-cpu-baseline
+      wait $sp ;;
     stream)
       python3 -c "import lzma; open('/tmp/C.tar','wb').write(lzma.decompress(open('tests/golden/C.tar.xz','rb').read()))"
       VS="$ROOT/bittorrent-with-congestion-control_amd/bin/verify-stream"

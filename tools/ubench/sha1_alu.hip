@@ -6,6 +6,7 @@
 // 2 = adds as VOP2 adds (no add3).
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #include "sha1_device.h"
 
@@ -118,7 +119,25 @@ void run(int waves_per_simd, int ops_per_block) {
   (void)hipFree(out); (void)hipFree(clk);
 }
 
-int main() {
+// `sha1_alu long N`: variant 0 at 2 waves/SIMD relaunched N times back to back
+// (a sustained run for power/clock sampling); prints the mean GB/s-equivalent.
+void run_long(int launches) {
+  const int blocks = 512, nb = 4000;
+  uint32_t *out; unsigned long long *clk;
+  (void)hipMalloc(&out, blocks * 256 * 4);
+  (void)hipMalloc(&clk, blocks * 16);
+  hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0);
+  for (int i = 0; i < launches; ++i) hipLaunchKernelGGL(kern<0>, dim3(blocks), dim3(256), 0, 0, out, clk, nb);
+  (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+  float ms; (void)hipEventElapsedTime(&ms, e0, e1);
+  printf("long: %d launches, %.3f ms each, %.0f GB/s-equivalent\n", launches, ms / launches,
+         (double)blocks * 256 * nb * 64 * launches / (ms * 1e-3) / 1e9);
+  (void)hipFree(out); (void)hipFree(clk);
+}
+
+int main(int argc, char **argv) {
+  if (argc > 2 && argv[1][0] == 'l') { run_long(atoi(argv[2])); return 0; }
   for (int rep = 0; rep < 2; ++rep)
     for (int w : {2, 4}) {
       run<0>(w, 613);

@@ -89,12 +89,21 @@ def cpu_baseline(host, n_chunks, gpu_digests, want_threads):
     tn = run(want_threads, n_chunks)
     ok = bytes(out) == gpu_digests[:20 * n_chunks]
     gib = n_chunks * CHUNK / 2**30
+    o0 = None  # the reference Makefile's own flags (-g, no -O): 1 thread, 32 chunks
+    ref0 = py_oracle.load_reference("O0")
+    if ref0 is not None:
+        n0 = min(n_chunks, 32)
+        o0_out = (ctypes.c_uint8 * 20)()
+        t0 = time.perf_counter()
+        for i in range(n0):
+            ref0.shahash(ctypes.c_void_p(base + i * CHUNK), CHUNK, o0_out)
+        o0 = round(n0 * CHUNK / 2**30 / (time.perf_counter() - t0), 4)
     return {
         "value": round(gib / tn, 4), "unit": "GiB/s", "cores": want_threads, "kind": kind,
         "sample": f"{n_chunks} x 512 KiB chunks ({gib:.1f} GiB) of the same synthetic workload, "
                   f"shahash per chunk, {want_threads} threads; 1 thread: "
                   f"{round(n1 * CHUNK / 2**30 / t1, 4)} GiB/s",
-        "flags": flags, "digests_match_gpu": ok,
+        "flags": flags, "digests_match_gpu": ok, "reference_O0_1thread_GiBs": o0,
         "host_cpu": _cpu_model(),
     }
 

@@ -23,6 +23,11 @@ run() {  # run NAME SECONDS CMD...
   esac
 }
 
+sampler() {  # sampler FILE N: board power + gfx clock once a second, N times
+  for i in $(seq 1 "$2"); do echo "T $(date +%T)"
+    timeout 10 amd-smi metric -g 0 -p -c 2>&1 | grep -E "SOCKET_POWER|GFX_0:" -A1; sleep 1; done > "$1" 2>&1
+}
+
 rocminfo 2>/dev/null | grep -m1 -E "gfx950" > "$OUT/device.txt" || true
 for step in "$@"; do
   case $step in
@@ -81,12 +86,16 @@ for step in "$@"; do
     residency) run residency 300 "$ROOT/tools/ubench/residency" ;;
     power_residency)
       # ~20 s per mode; power/clock sampled every second alongside
-      ( for i in $(seq 1 100); do echo "T $(date +%T)"; timeout 10 amd-smi metric -g 0 -p -c 2>&1 \
-          | grep -E "SOCKET_POWER|GFX_0:" -A1; sleep 1; done ) > "$OUT/power_residency_samples.log" 2>&1 &
+      sampler "$OUT/power_residency_samples.log" 100 &
       sp=$!
       run power_residency 300 "$ROOT/tools/ubench/residency" 131072 1000 1
       echo "T $(date +%T) alu_long start" >> "$OUT/power_residency_samples.log"
       run power_alu_long 300 "$ROOT/tools/ubench/sha1_alu" long 3000
+      wait $sp ;;
+    power_stream)
+      sampler "$OUT/power_stream_samples.log" 60 &
+      sp=$!
+      run power_stream 300 "$ROOT/tools/ubench/streamread" 400
       wait $sp ;;
     power)
       # sample board power and clocks while a ~30 s hot-kernel run is in flight

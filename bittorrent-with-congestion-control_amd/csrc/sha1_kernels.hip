@@ -51,6 +51,55 @@ __device__ __forceinline__ void compress_slot(State &st, const u32x4 (&q)[8 * L]
   }
 }
 
+// Shared tail of the fixed-layout kernels: whole blocks from `done` on (fewer
+// than one ring turn), the tail bytes + MD padding, the digest store and the
+// optional fused compare.
+template <bool VERIFY>
+__device__ __forceinline__ void epilogue(State &st, __amdgpu_buffer_rsrc_t rsrc, uint32_t voff, uint32_t done,
+                                         uint32_t len, uint32_t lane, uint32_t nvalid, uint64_t chunk0,
+                                         uint8_t *__restrict__ digests, const uint8_t *__restrict__ expected,
+                                         uint8_t *__restrict__ ok) {
+  const uint32_t nblocks = len >> 6;
+  for (uint32_t b = done; b < nblocks; ++b) {
+    uint32_t w[16];
+    const uint32_t o = b * 64u;
+    block_from_le(w, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o, 0),
+                  __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o + 16, 0),
+                  __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o + 32, 0),
+                  __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o + 48, 0));
+    compress(st, w);
+  }
+  // Tail bytes + MD padding (sha.c:536-543); r is uniform across the batch.
+  const uint32_t r = len & 63u;
+  uint32_t tail[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t have = r > 4u * j ? r - 4u * j : 0u;
+    uint32_t v = 0;
+    if (have) v = keep_be_bytes(bswap(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, nblocks * 64u + 4u * j, 0)), have);
+    tail[j] = v;
+  }
+  finish(st, tail, r, len);
+
+  if (lane < nvalid) {
+    const uint64_t idx = chunk0 + lane;
+    const uint32_t d0 = bswap(st.h0), d1 = bswap(st.h1), d2 = bswap(st.h2), d3 = bswap(st.h3), d4 = bswap(st.h4);
+    if (digests) {
+      uint32_t *o = (uint32_t *)(digests + idx * 20u);  // sha.c:550-553 big-endian bytes
+      o[0] = d0; o[1] = d1; o[2] = d2; o[3] = d3; o[4] = d4;
+    }
+    if constexpr (VERIFY) {  // util.c:311-313: memcmp(hash, chunk->hash, 20) == 0
+      const uint8_t *x = expected + idx * 20u;
+      uint32_t e[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        e[k] = (uint32_t)x[4 * k] | ((uint32_t)x[4 * k + 1] << 8) | ((uint32_t)x[4 * k + 2] << 16) |
+               ((uint32_t)x[4 * k + 3] << 24);
+      ok[idx] = (uint8_t)((e[0] == d0) & (e[1] == d1) & (e[2] == d2) & (e[3] == d3) & (e[4] == d4));
+    }
+  }
+}
+
 // NBUF ring slots of L lines; AUX = buffer-load cache policy (0 default, 2 nt).
 template <int NBUF, int L, int AUX, bool VERIFY>
 __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sha1_fixed(
@@ -95,45 +144,111 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
       }
     }
   }
-  // Remaining whole blocks (fewer than 2*L*NBUF), loaded directly.
-  for (uint32_t b = nmain * 2u * L; b < nblocks; ++b) {
-    uint32_t w[16];
-    const uint32_t o = b * 64u;
-    block_from_le(w, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o, 0),
-                  __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o + 16, 0),
-                  __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o + 32, 0),
-                  __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, o + 48, 0));
-    compress(st, w);
-  }
-  // Tail bytes + MD padding (sha.c:536-543); r is uniform across the batch.
-  const uint32_t r = len & 63u;
-  uint32_t tail[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t have = r > 4u * j ? r - 4u * j : 0u;
-    uint32_t v = 0;
-    if (have) v = keep_be_bytes(bswap(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, nblocks * 64u + 4u * j, 0)), have);
-    tail[j] = v;
-  }
-  finish(st, tail, r, len);
+  epilogue<VERIFY>(st, rsrc, voff, nmain * 2u * L, len, lane, nvalid, chunk0, digests, expected, ok);
+}
 
-  if (lane < nvalid) {
-    const uint64_t idx = chunk0 + lane;
-    const uint32_t d0 = bswap(st.h0), d1 = bswap(st.h1), d2 = bswap(st.h2), d3 = bswap(st.h3), d4 = bswap(st.h4);
-    if (digests) {
-      uint32_t *o = (uint32_t *)(digests + idx * 20u);  // sha.c:550-553 big-endian bytes
-      o[0] = d0; o[1] = d1; o[2] = d2; o[3] = d3; o[4] = d4;
-    }
-    if constexpr (VERIFY) {  // util.c:311-313: memcmp(hash, chunk->hash, 20) == 0
-      const uint8_t *x = expected + idx * 20u;
-      uint32_t e[5];
+// LDS-staged variant: the wave's 64 chunks are fetched COALESCED -- each
+// 16-byte load instruction moves 8 whole 128-byte lines (8 lanes per chunk
+// line) straight into LDS (buffer_load ... lds, no VGPR round trip) -- and
+// each lane then reads its own chunk's line back with ds_read_b128.  Same
+// bytes and VALU work as k_sha1_fixed, but the texture path handles 8 lines
+// per instruction instead of 64 (one per lane).  Per wave one 8 KiB slot
+// (64 rows x 128 B): slot s+1 is DMA'd while slot s (already in VGPRs) is
+// compressed.  Within a row the 16-byte pieces are rotated by (row/2) mod 8
+// so the 16 lanes of each ds_read_b128 pass hit distinct banks.
+//
+// The DMA is inline asm (hipcc neither orders builtin LDS-DMA against later
+// ds_reads of the same bytes nor counts it), so the waits are explicit:
+// vmcnt(0) before reading a slot, lgkmcnt(0) before overwriting it.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void glds_slot(const i32x4 rsrc, const uint32_t (&voff)[8], uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %10\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %9, %11 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %9, %11 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %9, %11 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %4, %9, %11 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %5, %9, %11 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %6, %9, %11 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %7, %9, %11 offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %8, %9, %11 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "v"(voff[4]), "v"(voff[5]), "v"(voff[6]),
+        "v"(voff[7]), "s"(rsrc), "s"(lds), "s"(soff)
+      : "memory", "scc");
+}
+
+template <bool VERIFY>
+__global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sha1_lds(
+    const uint8_t *__restrict__ base, uint64_t n_chunks, uint32_t pitch, uint32_t len, uint8_t *__restrict__ digests,
+    const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok) {
+  __shared__ u32x4 stage[kBlock / 64][64][8];  // [wave][row = chunk][16-byte piece, rotated]
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t chunk0 = (uint64_t)blockIdx.x * blockDim.x + (uint64_t)wave * 64u;
+  if (chunk0 >= n_chunks) return;
+  const uint64_t left = n_chunks - chunk0;
+  const uint32_t nvalid = left < 64 ? (uint32_t)left : 64u;
+  const uint32_t mine = lane < nvalid ? lane : nvalid - 1u;
+  const uint32_t voff = mine * pitch;
+  const uint32_t nrec = (nvalid - 1u) * pitch + ((len + 3u) & ~3u);
+  uint8_t *wbase = (uint8_t *)(base + chunk0 * (uint64_t)pitch);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(wbase, (short)0, (int)nrec, 0x00020000);
+  const uint64_t wb = (uint64_t)(uintptr_t)wbase;
+  const i32x4 rsrc4 = {(int)__builtin_amdgcn_readfirstlane((uint32_t)wb),
+                       (int)__builtin_amdgcn_readfirstlane((uint32_t)(wb >> 32) & 0xFFFFu),
+                       (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000};
+
+  // DMA instruction j, lane l: row q = 8j + l/8 (chunk min(q, nvalid-1)),
+  // position l%8 holds piece (l%8 + q/2) % 8 of the row's 128-byte line.
+  uint32_t dma_off[8];
 #pragma unroll
-      for (int k = 0; k < 5; ++k)
-        e[k] = (uint32_t)x[4 * k] | ((uint32_t)x[4 * k + 1] << 8) | ((uint32_t)x[4 * k + 2] << 16) |
-               ((uint32_t)x[4 * k + 3] << 24);
-      ok[idx] = (uint8_t)((e[0] == d0) & (e[1] == d1) & (e[2] == d2) & (e[3] == d3) & (e[4] == d4));
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t q = 8u * j + (lane >> 3);
+    const uint32_t src = q < nvalid ? q : nvalid - 1u;
+    dma_off[j] = src * pitch + (((lane & 7u) + (q >> 1)) & 7u) * 16u;
+  }
+  const uint32_t lds_wave = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)&stage[wave][0][0];
+  // Lane c reads piece p of row c at position (p - c/2) % 8.
+  const u32x4 *row = &stage[wave][lane][0];
+  const uint32_t rot = lane >> 1;
+
+  State st;
+  st.init();
+  const uint32_t nslots = (len >> 6) / 2u;  // 128-byte slots
+  if (nslots) {
+    glds_slot(rsrc4, dma_off, 0u, lds_wave);
+    for (uint32_t s = 0; s < nslots; ++s) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      u32x4 q[8];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) q[p] = row[(p - rot) & 7u];
+      if (s + 1 < nslots) glds_slot(rsrc4, dma_off, (s + 1) * 128u, lds_wave);  // waits lgkmcnt(0) first
+      __builtin_amdgcn_sched_barrier(0);
+      compress_slot<1>(st, q);
     }
   }
+  epilogue<VERIFY>(st, rsrc, voff, nslots * 2u, len, lane, nvalid, chunk0, digests, expected, ok);
 }
 
 // ---------------------------------------------------------------------------
@@ -327,11 +442,25 @@ static hipError_t launch_fixed_v(const void *d_in, uint64_t n, uint32_t pitch, u
   return hipGetLastError();
 }
 
+static hipError_t launch_lds(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
+                             const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s) {
+  const uint64_t grid = (n + kBlock - 1) / kBlock;
+  if (d_ok)
+    hipLaunchKernelGGL(k_sha1_lds<true>, dim3((uint32_t)grid), dim3(kBlock), 0, s, (const uint8_t *)d_in, n, pitch,
+                       len, d_dig, d_exp, d_ok);
+  else
+    hipLaunchKernelGGL(k_sha1_lds<false>, dim3((uint32_t)grid), dim3(kBlock), 0, s, (const uint8_t *)d_in, n, pitch,
+                       len, d_dig, d_exp, d_ok);
+  return hipGetLastError();
+}
+constexpr int kLdsVariant = 1010;  // bt_sha1_set_variant(10, 1, 0): LDS-staged k_sha1_lds
+
 // Variant code: NBUF*100 + L*10 + (nt ? 1 : 0).
 #define BT_FIXED_VARIANTS(X) X(2, 1, 0) X(3, 1, 0) X(4, 1, 0) X(2, 2, 0) \
   X(2, 1, 2) X(3, 1, 2) X(2, 2, 2)
 
 bool btsha1_fixed_variant_ok(int code) {
+  if (code == kLdsVariant) return true;
 #define BT_CASE(N, L, A) if (code == N * 100 + L * 10 + (A ? 1 : 0)) return true;
   BT_FIXED_VARIANTS(BT_CASE)
 #undef BT_CASE
@@ -341,6 +470,7 @@ bool btsha1_fixed_variant_ok(int code) {
 hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
                                const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant) {
   if (n == 0) return hipSuccess;
+  if (variant == kLdsVariant) return launch_lds(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
 #define BT_CASE(N, L, A) \
   if (variant == N * 100 + L * 10 + (A ? 1 : 0)) return launch_fixed_v<N, L, A>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
   BT_FIXED_VARIANTS(BT_CASE)

@@ -46,7 +46,8 @@ int bt_sha1_set_device(int device);
 const char *bt_sha1_last_error(void);
 /* Library / kernel build description (arch, ring depth). */
 const char *bt_sha1_build_info(void);
-/* Hot-kernel register-ring depth in 128-byte lines (2, 3 or 4; default 3). */
+/* Hot-kernel register-ring depth in 128-byte lines (2, 3 or 4; default 3).
+ * 10 selects the LDS-staged variant (coalesced loads DMA'd into LDS). */
 int bt_sha1_set_ring_depth(int nbuf);
 /* Hot-kernel variant: nbuf ring slots of `lines` 128-byte lines each, nt = 1
  * for non-temporal loads.  Returns -1 for a combination not compiled in. */

@@ -121,7 +121,10 @@ def synth4096(bt, torch, oracle):
     return buf
 
 
-@pytest.mark.parametrize("ring", [2, 3, 4])
+LDS = 10  # bt_sha1_set_ring_depth(10): the LDS-staged hot kernel (k_sha1_lds)
+
+
+@pytest.mark.parametrize("ring", [2, 3, 4, LDS])
 def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, ring):
     """BASELINE config 2: 4096 synthetic 512 KiB chunks, every digest == sha.c's."""
     bt.set_ring_depth(ring)
@@ -137,7 +140,16 @@ def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, ring):
         bt.set_ring_depth(3)
 
 
-def test_verify_dev_flags_mismatches(bt, torch, synth4096):
+@pytest.mark.parametrize("ring", [3, LDS])
+def test_verify_dev_flags_mismatches(bt, torch, synth4096, ring):
+    bt.set_ring_depth(ring)
+    try:
+        _verify_dev_flags_mismatches(bt, torch, synth4096)
+    finally:
+        bt.set_ring_depth(3)
+
+
+def _verify_dev_flags_mismatches(bt, torch, synth4096):
     n = 1000
     golden = read_pairs("synth4096.txt")[:n]
     exp = bytearray(b"".join(bytes.fromhex(h) for _, h in golden))
@@ -162,21 +174,26 @@ def test_verify_dev_flags_mismatches(bt, torch, synth4096):
     (1000, 1003, 67),            # odd pitch -> generic kernel
     (CHUNK, CHUNK + 256, 65),    # padded pitch, fast kernel
 ])
-def test_fixed_layouts_vs_oracle(bt, torch, oracle, chunk_len, pitch, n):
+@pytest.mark.parametrize("ring", [3, LDS])
+def test_fixed_layouts_vs_oracle(bt, torch, oracle, chunk_len, pitch, n, ring):
     total = pitch * (n - 1) + chunk_len
     host = bytearray(oracle.fill_synthetic(total, 11, 0xC0FFEE))
     d = to_dev(torch, bytes(host))
     out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
-    bt.chunks_dev(d.data_ptr(), n, chunk_len, pitch, out.data_ptr())
-    torch.cuda.synchronize()
+    bt.set_ring_depth(ring)
+    try:
+        bt.chunks_dev(d.data_ptr(), n, chunk_len, pitch, out.data_ptr())
+        torch.cuda.synchronize()
+    finally:
+        bt.set_ring_depth(3)
     want = [oracle.sha1(bytes(host[i * pitch:i * pitch + chunk_len])) for i in range(n)]
     assert digests_of(torch, out, n) == want
 
 
 def test_every_ring_depth_on_ragged_line_counts(bt, torch, oracle):
-    for ring in (2, 3, 4):
+    for ring in (2, 3, 4, LDS):
         bt.set_ring_depth(ring)
-        for blocks in range(0, 2 * 2 * ring + 3):
+        for blocks in range(0, 2 * 2 * min(ring, 4) + 3):
             for r in (0, 5, 56):
                 L = 64 * blocks + r
                 n = 70

@@ -97,6 +97,16 @@ for step in "$@"; do
       sp=$!
       run power_stream 300 "$ROOT/tools/ubench/streamread" 400
       wait $sp ;;
+    lds_ab)
+      for rep in 1 2; do
+        run "ab_ring3_$rep" 300 python3 bench.py --ring 3 --steps 20 --no-cpu-baseline
+        run "ab_lds_$rep" 300 python3 bench.py --ring 10 --steps 20 --no-cpu-baseline
+      done ;;
+    power_lds)
+      sampler "$OUT/power_lds_samples.log" 40 &
+      sp=$!
+      run power_lds 300 python3 bench.py --ring 10 --steps 1500 --warmup 3 --no-cpu-baseline
+      wait $sp ;;
     power)
       # sample board power and clocks while a ~30 s hot-kernel run is in flight
       ( for i in $(seq 1 12); do date +%T; timeout 10 amd-smi metric -g 0 -p -c 2>&1

@@ -162,43 +162,45 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
 // vmcnt(0) before reading a slot, lgkmcnt(0) before overwriting it.
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+#define BT_GLDS_ASM(POL)                                                                                \
+  asm volatile("s_waitcnt lgkmcnt(0)\n\t"                                                              \
+               "s_mov_b32 %0, m0\n\t"                                                                   \
+               "s_mov_b32 m0, %10\n\t"                                                                  \
+               "s_nop 0\n\t"                                                                            \
+               "buffer_load_dwordx4 %1, %9, %11 offen" POL " lds\n\t"                                   \
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"                                                 \
+               "buffer_load_dwordx4 %2, %9, %11 offen" POL " lds\n\t"                                   \
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"                                                 \
+               "buffer_load_dwordx4 %3, %9, %11 offen" POL " lds\n\t"                                   \
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"                                                 \
+               "buffer_load_dwordx4 %4, %9, %11 offen" POL " lds\n\t"                                   \
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"                                                 \
+               "buffer_load_dwordx4 %5, %9, %11 offen" POL " lds\n\t"                                   \
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"                                                 \
+               "buffer_load_dwordx4 %6, %9, %11 offen" POL " lds\n\t"                                   \
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"                                                 \
+               "buffer_load_dwordx4 %7, %9, %11 offen" POL " lds\n\t"                                   \
+               "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"                                                 \
+               "buffer_load_dwordx4 %8, %9, %11 offen" POL " lds\n\t"                                   \
+               "s_mov_b32 m0, %0"                                                                        \
+               : "=&s"(keep)                                                                             \
+               : "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "v"(voff[4]), "v"(voff[5]),     \
+                 "v"(voff[6]), "v"(voff[7]), "s"(rsrc), "s"(lds), "s"(soff)                              \
+               : "memory", "scc")
+
+// Eight DMA loads = one 8 KiB slot (64 rows x 128 B) at LDS byte address lds;
+// AUX 2 = non-temporal.  Waits for the wave's earlier ds_reads first (WAR).
+template <int AUX>
 __device__ __forceinline__ void glds_slot(const i32x4 rsrc, const uint32_t (&voff)[8], uint32_t soff, uint32_t lds) {
   uint32_t keep;
-  asm volatile(
-      "s_waitcnt lgkmcnt(0)\n\t"
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %10\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %9, %11 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %9, %11 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %3, %9, %11 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %4, %9, %11 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %5, %9, %11 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %6, %9, %11 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %7, %9, %11 offen lds\n\t"
-      "s_add_u32 m0, m0, 0x400\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %8, %9, %11 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "v"(voff[4]), "v"(voff[5]), "v"(voff[6]),
-        "v"(voff[7]), "s"(rsrc), "s"(lds), "s"(soff)
-      : "memory", "scc");
+  if constexpr (AUX == 2)
+    BT_GLDS_ASM(" nt");  // "offen nt lds"
+  else
+    BT_GLDS_ASM("");
 }
+#undef BT_GLDS_ASM
 
-template <bool VERIFY>
+template <int AUX, bool VERIFY>
 __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sha1_lds(
     const uint8_t *__restrict__ base, uint64_t n_chunks, uint32_t pitch, uint32_t len, uint8_t *__restrict__ digests,
     const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok) {
@@ -237,13 +239,13 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
   st.init();
   const uint32_t nslots = (len >> 6) / 2u;  // 128-byte slots
   if (nslots) {
-    glds_slot(rsrc4, dma_off, 0u, lds_wave);
+    glds_slot<AUX>(rsrc4, dma_off, 0u, lds_wave);
     for (uint32_t s = 0; s < nslots; ++s) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       u32x4 q[8];
 #pragma unroll
       for (int p = 0; p < 8; ++p) q[p] = row[(p - rot) & 7u];
-      if (s + 1 < nslots) glds_slot(rsrc4, dma_off, (s + 1) * 128u, lds_wave);  // waits lgkmcnt(0) first
+      if (s + 1 < nslots) glds_slot<AUX>(rsrc4, dma_off, (s + 1) * 128u, lds_wave);  // waits lgkmcnt(0) first
       __builtin_amdgcn_sched_barrier(0);
       compress_slot<1>(st, q);
     }
@@ -442,25 +444,27 @@ static hipError_t launch_fixed_v(const void *d_in, uint64_t n, uint32_t pitch, u
   return hipGetLastError();
 }
 
+template <int AUX>
 static hipError_t launch_lds(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
                              const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s) {
   const uint64_t grid = (n + kBlock - 1) / kBlock;
   if (d_ok)
-    hipLaunchKernelGGL(k_sha1_lds<true>, dim3((uint32_t)grid), dim3(kBlock), 0, s, (const uint8_t *)d_in, n, pitch,
+    hipLaunchKernelGGL((k_sha1_lds<AUX, true>), dim3((uint32_t)grid), dim3(kBlock), 0, s, (const uint8_t *)d_in, n, pitch,
                        len, d_dig, d_exp, d_ok);
   else
-    hipLaunchKernelGGL(k_sha1_lds<false>, dim3((uint32_t)grid), dim3(kBlock), 0, s, (const uint8_t *)d_in, n, pitch,
+    hipLaunchKernelGGL((k_sha1_lds<AUX, false>), dim3((uint32_t)grid), dim3(kBlock), 0, s, (const uint8_t *)d_in, n, pitch,
                        len, d_dig, d_exp, d_ok);
   return hipGetLastError();
 }
 constexpr int kLdsVariant = 1010;  // bt_sha1_set_variant(10, 1, 0): LDS-staged k_sha1_lds
+constexpr int kLdsNtVariant = 1011;  // bt_sha1_set_variant(10, 1, 1): the same with nt DMA loads
 
 // Variant code: NBUF*100 + L*10 + (nt ? 1 : 0).
 #define BT_FIXED_VARIANTS(X) X(2, 1, 0) X(3, 1, 0) X(4, 1, 0) X(2, 2, 0) \
   X(2, 1, 2) X(3, 1, 2) X(2, 2, 2)
 
 bool btsha1_fixed_variant_ok(int code) {
-  if (code == kLdsVariant) return true;
+  if (code == kLdsVariant || code == kLdsNtVariant) return true;
 #define BT_CASE(N, L, A) if (code == N * 100 + L * 10 + (A ? 1 : 0)) return true;
   BT_FIXED_VARIANTS(BT_CASE)
 #undef BT_CASE
@@ -470,7 +474,8 @@ bool btsha1_fixed_variant_ok(int code) {
 hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
                                const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant) {
   if (n == 0) return hipSuccess;
-  if (variant == kLdsVariant) return launch_lds(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
+  if (variant == kLdsVariant) return launch_lds<0>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
+  if (variant == kLdsNtVariant) return launch_lds<2>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
 #define BT_CASE(N, L, A) \
   if (variant == N * 100 + L * 10 + (A ? 1 : 0)) return launch_fixed_v<N, L, A>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
   BT_FIXED_VARIANTS(BT_CASE)

@@ -124,10 +124,11 @@ def synth4096(bt, torch, oracle):
 LDS = 10  # bt_sha1_set_ring_depth(10): the LDS-staged hot kernel (k_sha1_lds)
 
 
-@pytest.mark.parametrize("ring", [2, 3, 4, LDS])
-def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, ring):
-    """BASELINE config 2: 4096 synthetic 512 KiB chunks, every digest == sha.c's."""
-    bt.set_ring_depth(ring)
+@pytest.mark.parametrize("variant", [(2, 1, 0), (3, 1, 0), (4, 1, 0), (2, 2, 0), (3, 1, 1), (LDS, 1, 0), (LDS, 1, 1)])
+def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, variant):
+    """BASELINE config 2: 4096 synthetic 512 KiB chunks, every digest == sha.c's,
+    for every compiled hot-kernel variant (ring depth, slot lines, nt, LDS-staged)."""
+    bt.set_variant(*variant)
     try:
         n = 4096
         out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")

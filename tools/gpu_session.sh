@@ -101,6 +101,7 @@ for step in "$@"; do
       for rep in 1 2; do
         run "ab_ring3_$rep" 300 python3 bench.py --ring 3 --steps 20 --no-cpu-baseline
         run "ab_lds_$rep" 300 python3 bench.py --ring 10 --steps 20 --no-cpu-baseline
+        run "ab_ldsnt_$rep" 300 python3 bench.py --ring 10 --nt 1 --steps 20 --no-cpu-baseline
       done ;;
     power_lds)
       sampler "$OUT/power_lds_samples.log" 40 &

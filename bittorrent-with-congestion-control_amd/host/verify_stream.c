@@ -2,7 +2,7 @@
  * verify-stream -- the received-chunk verify path of the peer (util.c:250-337)
  * driven through the batched GPU verifier, end to end from host memory.
  *
- *   verify-stream [-b batch] [-s streams] [-r rounds] [-x] [-z] <data-file> <chunks-file>
+ *   verify-stream [-b batch] [-s streams] [-r rounds] [-p poll-every] [-x] [-z] <data-file> <chunks-file>
  *
  * For every chunk listed in <chunks-file> ("<id> <hex>" lines, as
  * parse_has_get_chunk_file reads them, util.c:90-93) the chunk's bytes are
@@ -16,7 +16,8 @@
  * receiver that lands DATA payloads directly in the pinned slots (recvfrom
  * into bt_sha1_verifier_slot() + offset): slots are written once, then every
  * later commit re-verifies the bytes already resident in its slot, so the
- * measured rate is the H2D + hash + D2H pipeline alone.  The last line is a
+ * measured rate is the H2D + hash + D2H pipeline alone.  -p N polls for
+ * verdicts after every N-th commit (default 1: after each chunk).  The last line is a
  * JSON summary with the host->verdict rate.
  */
 #include <fcntl.h>
@@ -54,20 +55,21 @@ static double now(void) {
 }
 
 int main(int argc, char **argv) {
-  int batch = 64, streams = 2, rounds = 1, corrupt = 0, zcopy = 0, opt;
-  while ((opt = getopt(argc, argv, "b:s:r:xz")) != -1) {
+  int batch = 64, streams = 2, rounds = 1, corrupt = 0, zcopy = 0, poll_every = 1, opt;
+  while ((opt = getopt(argc, argv, "b:s:r:p:xz")) != -1) {
     if (opt == 'b') batch = atoi(optarg);
     else if (opt == 's') streams = atoi(optarg);
     else if (opt == 'r') rounds = atoi(optarg);
     else if (opt == 'x') corrupt = 1;
     else if (opt == 'z') zcopy = 1;
+    else if (opt == 'p') poll_every = atoi(optarg) > 0 ? atoi(optarg) : 1;
     else {
-      fprintf(stderr, "usage: %s [-b batch] [-s streams] [-r rounds] [-x] <data-file> <chunks-file>\n", argv[0]);
+      fprintf(stderr, "usage: %s [-b batch] [-s streams] [-r rounds] [-p poll-every] [-x] [-z] <data-file> <chunks-file>\n", argv[0]);
       return 255;
     }
   }
   if (argc - optind != 2) {
-    fprintf(stderr, "usage: %s [-b batch] [-s streams] [-r rounds] [-x] <data-file> <chunks-file>\n", argv[0]);
+    fprintf(stderr, "usage: %s [-b batch] [-s streams] [-r rounds] [-p poll-every] [-x] [-z] <data-file> <chunks-file>\n", argv[0]);
     return 255;
   }
   int fd = open(argv[optind], O_RDONLY);
@@ -155,16 +157,18 @@ int main(int argc, char **argv) {
       }
       total++;
       timed++;
-      int m;
-      while ((m = bt_sha1_verifier_poll(v, out, 256)) > 0) count(out, m, &good, &bad);
+      if (total % poll_every == 0) {
+        int m;
+        while ((m = bt_sha1_verifier_poll(v, out, 256)) > 0) count(out, m, &good, &bad);
+      }
     }
   }
   int m;
   while ((m = bt_sha1_verifier_drain(v, out, 256)) > 0) count(out, m, &good, &bad);
   double dt = now() - t0;
   bt_sha1_verifier_destroy(v);
-  printf("{\"chunks\": %ld, \"ok\": %ld, \"failed\": %ld, \"seconds\": %.6f, \"GiB_per_s\": %.4f, \"batch\": %d, \"streams\": %d, \"mode\": \"%s\"}\n",
-         total, good, bad, dt, timed * (double)BT_CHUNK_SIZE / dt / (1u << 30), batch, streams,
+  printf("{\"chunks\": %ld, \"ok\": %ld, \"failed\": %ld, \"seconds\": %.6f, \"GiB_per_s\": %.4f, \"batch\": %d, \"streams\": %d, \"poll_every\": %d, \"mode\": \"%s\"}\n",
+         total, good, bad, dt, timed * (double)BT_CHUNK_SIZE / dt / (1u << 30), batch, streams, poll_every,
          zcopy ? "zero-copy slots" : "packetized memcpy (util.c:275)");
   return bad && !corrupt ? 1 : 0;
 }

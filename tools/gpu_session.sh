@@ -124,6 +124,18 @@ for step in "$@"; do
       run vs_zcopy_b1024_s2 300 "$VS" -z -b 1024 -s 2 -r 8 /tmp/C.tar tests/golden/ref_C.chunks
       run vs_zcopy_b2048_s3 300 "$VS" -z -b 2048 -s 3 -r 6 /tmp/C.tar tests/golden/ref_C.chunks
       run vs_zcopy_b256_s4 300 "$VS" -z -b 256 -s 4 -r 32 /tmp/C.tar tests/golden/ref_C.chunks ;;
+    stream_z)
+      python3 -c "import lzma; open('/tmp/C.tar','wb').write(lzma.decompress(open('tests/golden/C.tar.xz','rb').read()))"
+      VS="$ROOT/bittorrent-with-congestion-control_amd/bin/verify-stream"
+      run vsz_b2048_s3_p1 300 "$VS" -z -b 2048 -s 3 -r 6 /tmp/C.tar tests/golden/ref_C.chunks
+      run vsz_b2048_s3_p256 300 "$VS" -z -b 2048 -s 3 -r 6 -p 256 /tmp/C.tar tests/golden/ref_C.chunks
+      run vsz_b1024_s4_p256 300 "$VS" -z -b 1024 -s 4 -r 8 -p 256 /tmp/C.tar tests/golden/ref_C.chunks
+      run vsz_b4096_s3_p256 300 "$VS" -z -b 4096 -s 3 -r 4 -p 256 /tmp/C.tar tests/golden/ref_C.chunks ;;
+    vs_prof)
+      python3 -c "import lzma; open('/tmp/C.tar','wb').write(lzma.decompress(open('tests/golden/C.tar.xz','rb').read()))"
+      mkdir -p "$OUT/vs_prof"
+      run vs_prof 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/vs_prof" -o vs \
+        -- "$ROOT/bittorrent-with-congestion-control_amd/bin/verify-stream" -z -b 2048 -s 3 -r 6 /tmp/C.tar tests/golden/ref_C.chunks ;;
     stream_prof)
       mkdir -p "$OUT/stream_prof"
       run stream_prof 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/stream_prof" -o sb \

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -224,12 +225,26 @@ bool is_pinned(const void *p) {
 // the image (in lane.h_in, or in place when already pinned) and returns the
 // byte count (< max_bytes only at the end); sink(first_chunk, count, digests)
 // receives digests in chunk order.
+// BT_SHA1_TRACE=1: per-phase wall times of each pipeline run on stderr.
+bool trace_on() {
+  static const bool on = [] {
+    const char *e = getenv("BT_SHA1_TRACE");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 template <class Fill, class Sink>
 int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool staged, Fill fill, Sink sink) {
   if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
     set_err("chunk_len must be in [1, 4 GiB)");
     return -1;
   }
+  const double t_start = now_s();
+  double t_fill = 0, t_wait = 0;
   if (ensure_streams(c)) return -1;
   const uint64_t bytes_per = batch_bytes_for(chunk_len, size_hint);
   const uint64_t per = bytes_per / chunk_len;
@@ -238,9 +253,12 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
       return -1;
     l.busy = false;
   }
+  const double t_alloc = now_s() - t_start;
   auto drain = [&](Lane &l) -> int {
     if (!l.busy) return 0;
+    const double t0 = now_s();
     BT_CK(hipEventSynchronize(l.ev));
+    t_wait += now_s() - t0;
     sink(l.first, l.count, l.h_dig.as<uint8_t>());
     l.busy = false;
     return 0;
@@ -251,7 +269,9 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
     Lane &l = c->lane[k & 1];
     if (drain(l)) return -1;
     const uint8_t *src = nullptr;
+    const double t0 = now_s();
     int64_t got = fill(l, bytes_per, &src);
+    t_fill += now_s() - t0;
     if (got < 0) return -1;
     if (got == 0) break;
     const uint64_t cnt = ((uint64_t)got + chunk_len - 1) / chunk_len;
@@ -270,6 +290,11 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   }
   // Older lane first so digests arrive in order.
   if (drain(c->lane[k & 1]) || drain(c->lane[(k + 1) & 1])) return -1;
+  if (trace_on())
+    fprintf(stderr, "libbtsha1 pipeline dev %d: %llu chunks, batch %llu B, %s: total %.4f s = alloc %.4f + fill %.4f "
+                    "+ wait %.4f + other\n",
+            c->dev, (unsigned long long)next, (unsigned long long)bytes_per, staged ? "staged" : "direct DMA",
+            now_s() - t_start, t_alloc, t_fill, t_wait);
   return (int64_t)next;
 }
 

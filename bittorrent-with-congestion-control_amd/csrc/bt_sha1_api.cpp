@@ -28,6 +28,8 @@
 #include <vector>
 
 #include <sys/stat.h>
+#include <unistd.h>
+#include <cerrno>
 
 #include "bt_sha1.h"
 #include "chunk.h"
@@ -220,6 +222,72 @@ bool is_pinned(const void *p) {
   return a.type == hipMemoryTypeHost;
 }
 
+// Host staging threads for the pipelines' CPU side (memcpy into pinned memory,
+// file reads): one core moves ~8 GB/s, PCIe takes ~53.  BT_SHA1_COPY_THREADS
+// overrides the default of 8.
+int copy_threads() {
+  static const int n = [] {
+    const char *e = getenv("BT_SHA1_COPY_THREADS");
+    const int v = e ? atoi(e) : 8;
+    return v < 1 ? 1 : (v > 64 ? 64 : v);
+  }();
+  return n;
+}
+
+// Split [0, n) into page-aligned pieces of at least 16 MiB, one per thread
+// (the caller's thread takes the first), and run body(off, len, piece) on each.
+template <class Body>
+void parallel_pieces(uint64_t n, Body body) {
+  const uint64_t min_piece = 16ull << 20;
+  int t = copy_threads();
+  if ((uint64_t)t > n / min_piece) t = (int)std::max<uint64_t>(1, n / min_piece);
+  uint64_t piece = (n + t - 1) / t;
+  piece = (piece + 4095) & ~4095ull;
+  std::vector<std::thread> th;
+  for (int i = 1; i < t && (uint64_t)i * piece < n; ++i)
+    th.emplace_back([&, i] { body((uint64_t)i * piece, std::min<uint64_t>(piece, n - (uint64_t)i * piece), i); });
+  body(0, std::min<uint64_t>(piece, n), 0);
+  for (auto &x : th) x.join();
+}
+
+void parallel_copy(uint8_t *dst, const uint8_t *src, uint64_t n) {
+  if (n < (32ull << 20)) {
+    memcpy(dst, src, n);
+    return;
+  }
+  parallel_pieces(n, [&](uint64_t off, uint64_t len, int) { memcpy(dst + off, src + off, len); });
+}
+
+// pread `want` bytes at file offset `pos` into dst with several threads.
+// Returns the length of the contiguous prefix read (short only at EOF), or -1.
+int64_t parallel_pread(int fd, uint8_t *dst, uint64_t want, uint64_t pos) {
+  std::vector<int64_t> got(64, 0);
+  std::vector<uint64_t> asked(64, 0);
+  std::atomic<bool> err{false};
+  parallel_pieces(want, [&](uint64_t off, uint64_t len, int i) {
+    asked[i] = len;
+    uint64_t done = 0;
+    while (done < len) {
+      const ssize_t r = pread(fd, dst + off + done, (size_t)(len - done), (off_t)(pos + off + done));
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        err = true;
+        break;
+      }
+      if (r == 0) break;  // EOF
+      done += (uint64_t)r;
+    }
+    got[i] = (int64_t)done;
+  });
+  if (err) return -1;
+  int64_t total = 0;
+  for (int i = 0; i < 64 && asked[i]; ++i) {
+    total += got[i];
+    if ((uint64_t)got[i] < asked[i]) break;  // EOF inside piece i
+  }
+  return total;
+}
+
 // Generic double-buffered pipeline over two streams: batch k+1's H2D overlaps
 // batch k's hashing.  fill(lane, max_bytes, &src) provides up to max_bytes of
 // the image (in lane.h_in, or in place when already pinned) and returns the
@@ -248,12 +316,16 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   if (ensure_streams(c)) return -1;
   const uint64_t bytes_per = batch_bytes_for(chunk_len, size_hint);
   const uint64_t per = bytes_per / chunk_len;
-  for (auto &l : c->lane) {
-    if ((staged && l.h_in.ensure(bytes_per)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per))
-      return -1;
-    l.busy = false;
-  }
-  const double t_alloc = now_s() - t_start;
+  double t_alloc = 0;
+  // Buffers are sized (grow-only, kept across calls) when a lane is first
+  // used: an input that fits one batch never pins the second lane's memory.
+  auto prepare = [&](Lane &l) -> int {
+    const double t0 = now_s();
+    if ((staged && l.h_in.ensure(bytes_per)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per)) return -1;
+    t_alloc += now_s() - t0;
+    return 0;
+  };
+  for (auto &l : c->lane) l.busy = false;
   auto drain = [&](Lane &l) -> int {
     if (!l.busy) return 0;
     const double t0 = now_s();
@@ -267,7 +339,7 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   int k = 0;
   for (;;) {
     Lane &l = c->lane[k & 1];
-    if (drain(l)) return -1;
+    if (drain(l) || prepare(l)) return -1;
     const uint8_t *src = nullptr;
     const double t0 = now_s();
     int64_t got = fill(l, bytes_per, &src);
@@ -313,7 +385,7 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
     if (pinned) {
       *src = h_in + off;  // DMA straight from the caller's pinned image
     } else {
-      memcpy(l.h_in.p, h_in + off, n);
+      parallel_copy(l.h_in.as<uint8_t>(), h_in + off, n);
       *src = l.h_in.as<uint8_t>();
     }
     off += n;
@@ -334,11 +406,24 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
   }
   uint64_t hint = UINT64_MAX;
   struct stat st;
-  const long pos = ftell(fp);
-  if (fstat(fileno(fp), &st) == 0 && S_ISREG(st.st_mode) && pos >= 0 && st.st_size >= pos)
-    hint = (uint64_t)(st.st_size - pos);
+  const off_t pos = ftello(fp);
+  const bool regular = fstat(fileno(fp), &st) == 0 && S_ISREG(st.st_mode) && pos >= 0 && st.st_size >= pos;
+  if (regular) hint = (uint64_t)(st.st_size - pos);
+  uint64_t fpos = regular ? (uint64_t)pos : 0;
   auto fill = [&](Lane &l, uint64_t max, const uint8_t **src) -> int64_t {
-    // fread straight into pinned memory; short only at EOF (chunk.c:20).
+    *src = l.h_in.as<uint8_t>();
+    if (regular) {
+      // Regular file: several threads pread the batch straight into pinned
+      // memory at the FILE's logical position; short only at EOF.
+      const int64_t got = parallel_pread(fileno(fp), l.h_in.as<uint8_t>(), max, fpos);
+      if (got < 0) {
+        set_err("pread failed: %s", strerror(errno));
+        return -1;
+      }
+      fpos += (uint64_t)got;
+      return got;
+    }
+    // Pipe or device: fread to EOF as chunk.c:20 does.
     size_t got = 0;
     while (got < max) {
       size_t r = fread(l.h_in.as<uint8_t>() + got, 1, (size_t)(max - got), fp);
@@ -349,10 +434,18 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
       set_err("fread failed");
       return -1;
     }
-    *src = l.h_in.as<uint8_t>();
     return (int64_t)got;
   };
-  return run_pipeline(c, chunk_len, hint, true, fill, sink);
+  const int64_t n = run_pipeline(c, chunk_len, hint, true, fill, sink);
+  if (regular) {
+    // Leave the stream where the reference's fread loop leaves it: at EOF,
+    // with the end-of-file indicator set.
+    if (fseeko(fp, (off_t)fpos, SEEK_SET) == 0) {
+      const int ch = fgetc(fp);
+      if (ch != EOF) ungetc(ch, fp);
+    }
+  }
+  return n;
 }
 
 // Single message on the GPU (shahash): stage, ragged kernel, 20 bytes back.

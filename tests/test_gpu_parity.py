@@ -1,9 +1,11 @@
 """GPU parity: the HIP path (through the C-ABI) against the oracle and the
 reference's golden vectors.  Bit-exact everywhere (integer/byte work)."""
+import ctypes
 import hashlib
 import os
 import random
 import subprocess
+import threading
 
 import pytest
 
@@ -233,6 +235,72 @@ def test_make_chunks_file_api(bt, oracle, tmp_path):
     e = tmp_path / "empty"
     e.write_bytes(b"")
     assert bt.make_chunks_file(str(e)) == []
+
+
+def _libc():
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fdopen.restype = ctypes.c_void_p
+    libc.fdopen.argtypes = [ctypes.c_int, ctypes.c_char_p]
+    libc.fseek.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int]
+    libc.feof.argtypes = [ctypes.c_void_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    return libc
+
+
+def _chunks_fp(bt, fp, n):
+    out = (ctypes.c_uint8 * (20 * max(n, 1)))()
+    got = bt.lib.bt_sha1_chunks_file(ctypes.c_void_p(fp), CHUNK, out, n)
+    assert got >= 0, bt.last_error()
+    raw = bytes(out)
+    return [raw[20 * i:20 * i + 20] for i in range(got)]
+
+
+def test_file_path_threaded_reads_offsets_and_pipes(bt, oracle, tmp_path):
+    """The FILE* path reads regular files with parallel preads from the FILE's
+    logical position (several 16 MiB pieces per batch here) and leaves the
+    stream at EOF like chunk.c's fread loop; pipes go through fread."""
+    data = bytes(oracle.fill_synthetic(80 * 1024 * 1024 + 12345, 21, 0xF11E))
+    p = tmp_path / "big.bin"
+    p.write_bytes(data)
+    libc = _libc()
+    want = oracle.hash_chunks(data, CHUNK)
+    fp = libc.fopen(str(p).encode(), b"rb")
+    try:
+        assert _chunks_fp(bt, fp, len(want)) == want
+        assert libc.feof(fp) != 0
+    finally:
+        libc.fclose(fp)
+    off = 3 * CHUNK + 100  # a caller that already consumed part of the stream
+    fp = libc.fopen(str(p).encode(), b"rb")
+    try:
+        assert libc.fseek(fp, off, 0) == 0
+        assert _chunks_fp(bt, fp, len(want)) == oracle.hash_chunks(data[off:], CHUNK)
+        assert libc.feof(fp) != 0
+    finally:
+        libc.fclose(fp)
+    rfd, wfd = os.pipe()
+
+    def writer():
+        with os.fdopen(wfd, "wb") as w:
+            w.write(data)
+
+    t = threading.Thread(target=writer)
+    t.start()
+    fp = libc.fdopen(rfd, b"rb")
+    try:
+        assert _chunks_fp(bt, fp, len(want)) == want
+    finally:
+        libc.fclose(fp)
+        t.join()
+
+
+def test_chunks_host_pageable_parallel_staging(bt, oracle):
+    """Pageable input > 32 MiB: the staging copy into pinned memory is split
+    over threads; digests unchanged."""
+    data = bytes(oracle.fill_synthetic(96 * 1024 * 1024 + 999, 22, 0xF11F))
+    assert bt.chunks_host(data) == oracle.hash_chunks(data, CHUNK)
 
 
 def test_make_chunks_cli(tmp_path, oracle):

@@ -203,11 +203,16 @@ int launch_image(const uint8_t *d_img, uint64_t bytes, uint64_t chunk_len, uint8
 
 // Staging batch: ~1 GiB per lane keeps >= 2048 chunks in flight per launch,
 // enough that the per-chunk hash latency (~10 ms, 8193 dependent blocks at one
-// wave per SIMD) still outruns PCIe; capped by the input size when known.
+// wave per SIMD) still outruns PCIe; capped by the input size when known.  An
+// input of 64 MiB - 2 GiB is cut in two batches so both lanes work (the second
+// lane's pinning overlaps the first batch, see run_pipeline).
 uint64_t batch_bytes_for(uint64_t chunk_len, uint64_t size_hint) {
   const uint64_t target = 1ull << 30;
   uint64_t per = std::max<uint64_t>(1, target / chunk_len);
-  if (size_hint != UINT64_MAX) per = std::max<uint64_t>(1, std::min<uint64_t>(per, (size_hint + chunk_len - 1) / chunk_len));
+  if (size_hint != UINT64_MAX) {
+    const uint64_t n = (size_hint + chunk_len - 1) / chunk_len;
+    per = std::max<uint64_t>(1, std::min<uint64_t>(per, size_hint >= (64ull << 20) ? (n + 1) / 2 : n));
+  }
   return per * chunk_len;
 }
 

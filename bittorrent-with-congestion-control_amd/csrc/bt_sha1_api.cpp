@@ -294,10 +294,12 @@ int64_t parallel_pread(int fd, uint8_t *dst, uint64_t want, uint64_t pos) {
 }
 
 // Generic double-buffered pipeline over two streams: batch k+1's H2D overlaps
-// batch k's hashing.  fill(lane, max_bytes, &src) provides up to max_bytes of
-// the image (in lane.h_in, or in place when already pinned) and returns the
-// byte count (< max_bytes only at the end); sink(first_chunk, count, digests)
-// receives digests in chunk order.
+// batch k's hashing, and inside a batch each 128 MiB piece is copied to the
+// device as soon as it is staged, so host reads overlap the H2D.
+// fill(lane, off, max_bytes, &src) provides up to max_bytes of the image at
+// byte `off` of the lane's batch (staged at lane.h_in + off, or in place when
+// already pinned) and returns the byte count (< max_bytes only at the end);
+// sink(first_chunk, count, digests) receives digests in chunk order.
 // BT_SHA1_TRACE=1: per-phase wall times of each pipeline run on stderr.
 bool trace_on() {
   static const bool on = [] {
@@ -309,6 +311,8 @@ bool trace_on() {
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+
+constexpr uint64_t kPiece = 128ull << 20;  // staging -> H2D granule inside a batch
 
 template <class Fill, class Sink>
 int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool staged, Fill fill, Sink sink) {
@@ -376,25 +380,32 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   for (;;) {
     Lane &l = c->lane[k & 1];
     if ((k == 1 && join_pre()) || drain(l) || prepare(l)) return -1;
-    const uint8_t *src = nullptr;
-    const double t0 = now_s();
-    int64_t got = fill(l, bytes_per, &src);
-    t_fill += now_s() - t0;
-    if (got < 0) return -1;
+    uint64_t got = 0;
+    bool eof = false;
+    while (got < bytes_per) {
+      const uint64_t want = std::min<uint64_t>(kPiece, bytes_per - got);
+      const uint8_t *src = nullptr;
+      const double t0 = now_s();
+      const int64_t r = fill(l, got, want, &src);
+      t_fill += now_s() - t0;
+      if (r < 0) return -1;
+      if (r) BT_CK(hipMemcpyAsync(l.d_in.as<uint8_t>() + got, src, (size_t)r, hipMemcpyHostToDevice, l.s));
+      got += (uint64_t)r;
+      if ((uint64_t)r < want) {
+        eof = true;
+        break;
+      }
+    }
     if (got == 0) break;
-    const uint64_t cnt = ((uint64_t)got + chunk_len - 1) / chunk_len;
-    BT_CK(hipMemcpyAsync(l.d_in.p, src, (size_t)got, hipMemcpyHostToDevice, l.s));
-    // Digests go straight to pinned host memory from the kernel: a D2H copy
-    // here would sit in the shared copy-engine queue behind this batch's
-    // kernel and hold up the next batch's H2D (measured: full serialisation).
-    if (launch_image(l.d_in.as<uint8_t>(), (uint64_t)got, chunk_len, l.h_dig.as<uint8_t>(), l.s)) return -1;
+    const uint64_t cnt = (got + chunk_len - 1) / chunk_len;
+    if (launch_image(l.d_in.as<uint8_t>(), got, chunk_len, l.h_dig.as<uint8_t>(), l.s)) return -1;
     BT_CK(hipEventRecord(l.ev, l.s));
     l.busy = true;
     l.first = next;
     l.count = cnt;
     next += cnt;
     ++k;
-    if ((uint64_t)got < bytes_per) break;
+    if (eof) break;
   }
   if (join_pre()) return -1;  // input shorter than the size hint
   // Older lane first so digests arrive in order.
@@ -417,17 +428,18 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   }
   const bool pinned = is_pinned(h_in);
   uint64_t off = 0;
-  auto fill = [&](Lane &l, uint64_t max, const uint8_t **src) -> int64_t {
+  auto fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src) -> int64_t {
     const uint64_t n = std::min<uint64_t>(max, total - off);
     if (pinned) {
       *src = h_in + off;  // DMA straight from the caller's pinned image
     } else {
-      parallel_copy(l.h_in.as<uint8_t>(), h_in + off, n);
-      *src = l.h_in.as<uint8_t>();
+      parallel_copy(l.h_in.as<uint8_t>() + at, h_in + off, n);
+      *src = l.h_in.as<uint8_t>() + at;
     }
     off += n;
     return (int64_t)n;
   };
+
   auto sink = [&](uint64_t first, uint64_t count, const uint8_t *d) { memcpy(h_dig + 20 * first, d, 20 * count); };
   return run_pipeline(c, chunk_len, total, !pinned, fill, sink);
 }
@@ -447,12 +459,13 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
   const bool regular = fstat(fileno(fp), &st) == 0 && S_ISREG(st.st_mode) && pos >= 0 && st.st_size >= pos;
   if (regular) hint = (uint64_t)(st.st_size - pos);
   uint64_t fpos = regular ? (uint64_t)pos : 0;
-  auto fill = [&](Lane &l, uint64_t max, const uint8_t **src) -> int64_t {
-    *src = l.h_in.as<uint8_t>();
+  auto fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src) -> int64_t {
+    uint8_t *dst = l.h_in.as<uint8_t>() + at;
+    *src = dst;
     if (regular) {
       // Regular file: several threads pread the batch straight into pinned
       // memory at the FILE's logical position; short only at EOF.
-      const int64_t got = parallel_pread(fileno(fp), l.h_in.as<uint8_t>(), max, fpos);
+      const int64_t got = parallel_pread(fileno(fp), dst, max, fpos);
       if (got < 0) {
         set_err("pread failed: %s", strerror(errno));
         return -1;
@@ -463,7 +476,7 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
     // Pipe or device: fread to EOF as chunk.c:20 does.
     size_t got = 0;
     while (got < max) {
-      size_t r = fread(l.h_in.as<uint8_t>() + got, 1, (size_t)(max - got), fp);
+      size_t r = fread(dst + got, 1, (size_t)(max - got), fp);
       if (r == 0) break;
       got += r;
     }

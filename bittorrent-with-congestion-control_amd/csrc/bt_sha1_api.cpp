@@ -383,7 +383,10 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
     uint64_t got = 0;
     bool eof = false;
     while (got < bytes_per) {
-      const uint64_t want = std::min<uint64_t>(kPiece, bytes_per - got);
+      // Staged input moves in pieces (host reads overlap the H2D); pinned
+      // input goes as one copy per batch -- 128 MiB copies straight from
+      // registered memory measured 36.5 GiB/s against 50 for 1 GiB ones.
+      const uint64_t want = std::min<uint64_t>(staged ? kPiece : bytes_per, bytes_per - got);
       const uint8_t *src = nullptr;
       const double t0 = now_s();
       const int64_t r = fill(l, got, want, &src);

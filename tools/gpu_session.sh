@@ -103,6 +103,11 @@ for step in "$@"; do
         run "ab_lds_$rep" 300 python3 bench.py --ring 10 --steps 20 --no-cpu-baseline
         run "ab_ldsnt_$rep" 300 python3 bench.py --ring 10 --nt 1 --steps 20 --no-cpu-baseline
       done ;;
+    power_valu)
+      sampler "$OUT/power_valu_samples.log" 50 &
+      sp=$!
+      run power_valu 300 "$ROOT/tools/ubench/valu_energy" 4
+      wait $sp ;;
     power_lds)
       sampler "$OUT/power_lds_samples.log" 40 &
       sp=$!

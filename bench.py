@@ -84,15 +84,15 @@ def cpu_baseline(host, n_chunks, gpu_digests, want_threads):
             t.join()
         return time.perf_counter() - t0
 
-    n1 = min(n_chunks, 128)
+    n1 = min(n_chunks, 2048)  # ~1.5 s on one core
     t1 = run(1, n1)
     tn = run(want_threads, n_chunks)
     ok = bytes(out) == gpu_digests[:20 * n_chunks]
     gib = n_chunks * CHUNK / 2**30
-    o0 = None  # the reference Makefile's own flags (-g, no -O): 1 thread, 32 chunks
+    o0 = None  # the reference Makefile's own flags (-g, no -O): 1 thread, 256 chunks
     ref0 = py_oracle.load_reference("O0")
     if ref0 is not None:
-        n0 = min(n_chunks, 32)
+        n0 = min(n_chunks, 256)
         o0_out = (ctypes.c_uint8 * 20)()
         t0 = time.perf_counter()
         for i in range(n0):
@@ -129,7 +129,8 @@ def main():
     ap.add_argument("--nt", type=int, default=0, help="non-temporal loads (with --ring)")
     ap.add_argument("--pitch", type=int, default=CHUNK, help="bytes between chunk starts in HBM")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-chunks", type=int, default=8192)
+    ap.add_argument("--cpu-chunks", type=int, default=32768,
+                    help="CPU-baseline sample: 16 GiB, ~25 core-seconds of reference sha.c")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo for rehearsals)")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r01.json"))
@@ -245,7 +246,9 @@ def main():
         import numpy as np
         host = np.empty(n * CHUNK, dtype=np.uint8)
         if pitch == CHUNK:
-            host[:] = buf[:n * CHUNK].cpu().numpy()
+            step = 2048 * CHUNK  # 1 GiB slices: no second full-size host copy
+            for o in range(0, n * CHUNK, step):
+                host[o:o + step] = buf[o:min(o + step, n * CHUNK)].cpu().numpy()
         else:
             for i in range(n):
                 host[i * CHUNK:(i + 1) * CHUNK] = buf[i * pitch:i * pitch + CHUNK].cpu().numpy()

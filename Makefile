@@ -71,6 +71,20 @@ $(ASANDIR)/libbtsha1.so: $(CSRC)/bt_sha1_api.cpp $(CSRC)/bt_chunks.cpp $(PKG)/bu
 $(ASANDIR)/host_stress: tests/native/host_stress.c $(ASANDIR)/libbtsha1.so
 	/opt/rocm/llvm/bin/clang -g -O1 -fsanitize=address,undefined -fno-omit-frame-pointer -Iinclude -o $@ $< -L$(ASANDIR) -lbtsha1 -Wl,-rpath,'$$ORIGIN'
 
+# Scheduler-strategy builds of the library (experiment in profiles/r01/experiments.md;
+# tools/gpu_session.sh libvariants benches each).  Not part of the product.
+SCHED_default :=
+SCHED_maxilp  := -mllvm -amdgpu-sched-strategy=max-ilp
+SCHED_iterilp := -mllvm -amdgpu-sched-strategy=iterative-ilp
+SCHED_maxmem  := -mllvm -amdgpu-sched-strategy=max-memory-clause
+SCHED_bias0   := -mllvm -amdgpu-schedule-metric-bias=0
+SCHED_NAMES   := default maxilp iterilp maxmem bias0
+sched_variants: $(foreach v,$(SCHED_NAMES),build_variants/$(v)/libbtsha1.so)
+build_variants/%/libbtsha1.so: $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) $(SCHED_$*) -c $< -o $(dir $@)sha1_kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(dir $@)sha1_kernels.o $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o -Wl,-soname,libbtsha1.so
+
 # Microbenchmarks behind the measurements in profiles/ (not part of the product).
 UB_SRC := $(wildcard tools/ubench/*.hip)
 UB_BIN := $(UB_SRC:.hip=) tools/ubench/residency
@@ -84,4 +98,4 @@ clean:
 	rm -rf $(PKG)/build $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib tools oracle dropin asan ubench clean
+.PHONY: all lib tools oracle dropin asan ubench sched_variants clean

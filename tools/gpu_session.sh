@@ -52,9 +52,10 @@ for step in "$@"; do
     ubench_alu) run ubench_alu 300 "$ROOT/tools/ubench/sha1_alu" ;;
     mixpattern) run mixpattern 300 "$ROOT/tools/ubench/mixpattern" ;;
     libvariants)
+      make -C "$ROOT" -j16 sched_variants > "$OUT/sched_variants_build.log" 2>&1 || exit 2
       for rep in 1 2; do
-        for d in "$ROOT"/build_variants/*/; do
-          n=$(basename "$d")
+        for n in default maxilp iterilp maxmem bias0; do
+          d="$ROOT/build_variants/$n"
           run "libvar_${n}_$rep" 300 env BT_SHA1_LIB="$d/libbtsha1.so" python3 bench.py --steps 10 --no-cpu-baseline
         done
       done ;;

@@ -114,6 +114,11 @@ for step in "$@"; do
       sp=$!
       run power_lds 300 python3 bench.py --ring 10 --steps 1500 --warmup 3 --no-cpu-baseline
       wait $sp ;;
+    power_stream2)
+      sampler "$OUT/power_stream2_samples.log" 90 &
+      sp=$!
+      run power_stream2 300 "$ROOT/tools/ubench/streamread2" 400
+      wait $sp ;;
     power)
       # sample board power and clocks while a ~30 s hot-kernel run is in flight
       ( for i in $(seq 1 12); do date +%T; timeout 10 amd-smi metric -g 0 -p -c 2>&1

@@ -19,6 +19,15 @@
                op " v[52:53], 5, v[54:55]\n\t" op " v[56:57], 5, v[58:59]\n\t" op " v[60:61], 5, v[62:63]\n\t"
 #define PKMOV(op) op " v[40:41], v[42:43], v[44:45] op_sel:[1,0]\n\t" op " v[46:47], v[48:49], v[50:51] op_sel:[1,0]\n\t" op " v[52:53], v[54:55], v[56:57] op_sel:[1,0]\n\t" \
                op " v[58:59], v[60:61], v[62:63] op_sel:[1,0]\n\t" op " v[40:41], v[48:49], v[56:57] op_sel:[1,0]\n\t" op " v[46:47], v[54:55], v[62:63] op_sel:[1,0]\n\t"
+// the rotate form the SHA-1 rounds use: both data sources the same register, constant shift
+#define ROT(n) "v_alignbit_b32 v40, v41, v41, " #n "\n\tv_alignbit_b32 v44, v45, v45, " #n "\n\tv_alignbit_b32 v48, v49, v49, " #n "\n\t" \
+               "v_alignbit_b32 v52, v53, v53, " #n "\n\tv_alignbit_b32 v56, v57, v57, " #n "\n\tv_alignbit_b32 v60, v61, v61, " #n "\n\t"
+// two of three sources in one bank (v41/v45/v49/v53/v57/v61 are bank 1; v42.. bank 2)
+#define SB2(op) op " v40, v41, v45, v42\n\t" op " v44, v49, v53, v46\n\t" op " v48, v57, v61, v50\n\t" op " v52, v41, v49, v54\n\t" \
+                op " v56, v45, v53, v58\n\t" op " v60, v57, v41, v62\n\t"
+// two-source VOP2: same bank vs distinct banks
+#define X2S(op) op " v40, v41, v45\n\t" op " v44, v49, v53\n\t" op " v48, v57, v61\n\t" op " v52, v41, v49\n\t" op " v56, v45, v53\n\t" op " v60, v57, v41\n\t"
+#define X2D(op) op " v40, v41, v42\n\t" op " v44, v45, v46\n\t" op " v48, v49, v50\n\t" op " v52, v53, v54\n\t" op " v56, v57, v58\n\t" op " v60, v61, v62\n\t"
 #define MOV(op) op " v40, v41\n\t" op " v44, v45\n\t" op " v48, v49\n\t" op " v52, v53\n\t" op " v56, v57\n\t" op " v60, v61\n\t"
 #define ADDCO(op) op " v40, vcc, v41, v42\n\t" op " v44, vcc, v45, v46\n\t" op " v48, vcc, v49, v50\n\t" op " v52, vcc, v53, v54\n\t" op " v56, vcc, v57, v58\n\t" op " v60, vcc, v61, v62\n\t"
 
@@ -39,6 +48,10 @@ __global__ __launch_bounds__(256) void kern(uint32_t *out, int iters) {
     if constexpr (P == 9) asm volatile(MOV("v_mov_b32") MOV("v_mov_b32") MOV("v_mov_b32") MOV("v_mov_b32") ::: CLOB);
     if constexpr (P == 10) asm volatile(ADDCO("v_add_co_u32") ADDCO("v_add_co_u32") ADDCO("v_add_co_u32") ADDCO("v_add_co_u32") ::: CLOB, "vcc");
     if constexpr (P == 5) asm volatile(SB("v_alignbit_b32") SB("v_alignbit_b32") SB("v_alignbit_b32") SB("v_alignbit_b32") ::: CLOB);
+    if constexpr (P == 12) asm volatile(SB2("v_bitop3_b32") SB2("v_bitop3_b32") SB2("v_bitop3_b32") SB2("v_bitop3_b32") ::: CLOB);
+    if constexpr (P == 13) asm volatile(X2S("v_xor_b32") X2S("v_xor_b32") X2S("v_xor_b32") X2S("v_xor_b32") ::: CLOB);
+    if constexpr (P == 14) asm volatile(X2D("v_xor_b32") X2D("v_xor_b32") X2D("v_xor_b32") X2D("v_xor_b32") ::: CLOB);
+    if constexpr (P == 11) asm volatile(ROT(27) ROT(2) ROT(31) ROT(27) ::: CLOB);
   }
   uint32_t r;
   asm volatile("v_xor_b32 %0, v40, v44\n\tv_xor_b32 %0, %0, v48" : "=v"(r) :: CLOB);
@@ -68,7 +81,15 @@ void run(const char *name, int w) {
 int main() {
   for (int w : {2, 8}) {
     run<0>("add3 distinct banks", w);
+    run<1>("add3 same bank", w);
     run<2>("bitop3 distinct banks", w);
+    run<3>("bitop3 same bank", w);
+    run<12>("bitop3 two in one bank", w);
+    run<13>("xor same bank", w);
+    run<14>("xor distinct banks", w);
+    run<4>("alignbit distinct banks", w);
+    run<5>("alignbit same bank", w);
+    run<11>("alignbit x,x,const (rotl)", w);
     run<6>("v_lshl_add_u64", w);
     run<7>("v_lshlrev_b64", w);
     run<8>("v_pk_mov_b32", w);

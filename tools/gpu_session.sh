@@ -119,6 +119,7 @@ for step in "$@"; do
       sp=$!
       run power_stream2 300 "$ROOT/tools/ubench/streamread2" 400
       wait $sp ;;
+    wgdist) run wgdist 120 "$ROOT/tools/ubench/wgdist" ;;
     power)
       # sample board power and clocks while a ~30 s hot-kernel run is in flight
       ( for i in $(seq 1 12); do date +%T; timeout 10 amd-smi metric -g 0 -p -c 2>&1

@@ -93,3 +93,26 @@ def test_reference_callers_compile_and_link_against_dropin(tmp_path):
     subprocess.run(["gcc", "-Wall", "-I", os.path.join(REPO, "include"), "-o", str(exe), src,
                     f"-L{PKG}", "-lbtsha1", "-lm", f"-Wl,-rpath,{PKG}"], check=True, capture_output=True)
     assert exe.exists()
+
+
+def test_integration_peer_example_compiles(tmp_path):
+    """The batched-verify snippet of INTEGRATION.md §3 compiles and links against
+    include/ + libbtsha1.so as written (guards the documented calls against drift)."""
+    import re
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    sec = text[text.index("## 3."):]
+    body = re.search(r"```c\n(.*?)```", sec, re.S).group(1)
+    body = "\n".join(l for l in body.splitlines() if not l.startswith("#include"))
+    src = tmp_path / "peer_example.c"
+    src.write_text(
+        "#include <stdint.h>\n#include \"bt_sha1.h\"\n#include \"chunk.h\"\n"
+        "enum { NOT_STARTED, RECEIVING, VERIFYING, OWNED };\n"
+        "struct Chunk { int state; char *data; uint32_t received_byte_number; uint8_t hash[20]; };\n"
+        "struct Request { struct Chunk chunks[4]; };\n"
+        "void peer_example(struct Chunk *chunk, int chunk_id, struct Request *current_request) {\n"
+        + body + "\n}\nint main(void) { return 0; }\n")
+    exe = tmp_path / "peer_example"
+    r = subprocess.run(["gcc", "-Wall", "-Wno-unused-variable", "-Werror", "-I", os.path.join(REPO, "include"),
+                        "-o", str(exe), str(src), f"-L{PKG}", "-lbtsha1", f"-Wl,-rpath,{PKG}"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

@@ -32,14 +32,14 @@ PKG = os.path.join(HERE, "bittorrent-with-congestion-control_amd")
 CHUNK = 512 * 1024
 SEED = 0x0B175EED
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
-VALU_OPS_PER_BLOCK = 613       # counted in the kernel's ISA
+VALU_OPS_PER_BLOCK = 597       # counted in the kernel's ISA
 VALU_HALF_RATE_PER_BLOCK = 400  # v_alignbit / v_add3 / v_perm: 16 lanes/clk/SIMD (tools/ubench)
-VALU_FULL_RATE_PER_BLOCK = 213  # v_bitop3 / v_xor / v_add: 32 lanes/clk/SIMD with co-issue
+VALU_FULL_RATE_PER_BLOCK = 197  # v_bitop3 / v_xor / v_add: 32 lanes/clk/SIMD with co-issue
 SIMDS, CLOCK_GHZ = 1024, 2.4
 # VALU ceiling for this exact instruction mix: a wave64 half-rate op holds the
-# SIMD 4 clocks, a full-rate op 2 -> 2026 clocks per 64-byte block per wave.
+# SIMD 4 clocks, a full-rate op 2 -> 1994 clocks per 64-byte block per wave.
 _MIX_CLK = 4 * VALU_HALF_RATE_PER_BLOCK + 2 * VALU_FULL_RATE_PER_BLOCK
-VALU_MIX_PEAK_TOPS = VALU_OPS_PER_BLOCK * 64 * SIMDS * CLOCK_GHZ * 1e9 / _MIX_CLK / 1e12  # lane-ops/s, ~47.5
+VALU_MIX_PEAK_TOPS = VALU_OPS_PER_BLOCK * 64 * SIMDS * CLOCK_GHZ * 1e9 / _MIX_CLK / 1e12  # lane-ops/s, ~47.1
 
 
 def load_btsha1():
@@ -285,7 +285,8 @@ def main():
         "valu_roofline": {"bound": "valu", "achieved": round(valu_tops, 2), "peak": round(VALU_MIX_PEAK_TOPS, 2),
                           "unit": "T int32 lane-ops/s", "frac": round(valu_tops / VALU_MIX_PEAK_TOPS, 4),
                           "ops_per_block": VALU_OPS_PER_BLOCK,
-                          "peak_basis": "613-instruction mix (400 half-rate, 213 full-rate) at 2.4 GHz on 1024 SIMDs"},
+                          "peak_basis": f"{VALU_OPS_PER_BLOCK}-instruction mix ({VALU_HALF_RATE_PER_BLOCK} half-rate, "
+                                        f"{VALU_FULL_RATE_PER_BLOCK} full-rate) at 2.4 GHz on 1024 SIMDs"},
         "parity_first_4096_vs_golden": parity,
         "cpu_baseline": cpu,
     }

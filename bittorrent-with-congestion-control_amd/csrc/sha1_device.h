@@ -9,8 +9,11 @@
 //     Ch = 0xCA, Parity = 0x96, Maj = 0xE8 over (b, c, d);
 //   * ROTL (sha.c:49) is v_alignbit_b32, BYTESWAP (sha.c:80-81) is v_perm_b32,
 //     and the five-term sum of DO_ROUND (sha.c:57-64) is two v_add3_u32.
-// Per 64-byte block: 80 x 5 round ops + 64 x 3 schedule ops + 16 byte swaps +
-// 5 state adds = 613 VALU instructions; no memory traffic besides the block.
+//   * the schedule shares 16 XOR pairs between words 16..31 and 64..79 via the
+//     recurrence squared twice (sched_pair below).
+// Per 64-byte block: 80 x 5 round ops + 176 schedule ops (48 x 3 + 16 x 2) +
+// 16 byte swaps + 5 state adds = 597 VALU instructions (613 with the plain
+// recurrence); no memory traffic besides the block.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -87,10 +90,43 @@ __device__ __forceinline__ void rounds_from(uint32_t (&w)[16], uint32_t &a, uint
   }
 }
 
+// Schedule with shared pairs (597 instead of 613 VALU per block; measured
+// +1.4 % on the power-capped hot kernel, profiles/r01/experiments.md).  The
+// recurrence squared twice over GF(2) gives, for t >= 64,
+//   W[t] = ROTL4(W[t-12] ^ W[t-32] ^ W[t-56] ^ W[t-64]),
+// and its pair W[t-64] ^ W[t-56] = W[i] ^ W[i+8] (i = t-64) is exactly the
+// pair W[t'-16] ^ W[t'-8] that word t' = i+16 needs.  So words 16..31 keep
+// their pair P[i] and words 64..79 cost bitop3 + rotate instead of
+// xor + bitop3 + rotate.  Q[i] = W[32+i] stays live for those words too
+// (~32 VGPRs more; occupancy is set by the chunk count, not registers).
+template <int T>
+__device__ __forceinline__ uint32_t sched_pair(uint32_t (&w)[16], uint32_t (&p)[16], uint32_t (&q)[16]) {
+  if constexpr (T >= 16 && T < 32) {
+    p[T - 16] = w[T & 15] ^ w[(T - 8) & 15];
+    w[T & 15] = rotl(__builtin_amdgcn_bitop3_b32(p[T - 16], w[(T - 3) & 15], w[(T - 14) & 15], 0x96), 1);
+  } else if constexpr (T >= 32 && T < 64) {
+    sched<T>(w);
+    if constexpr (T < 48) q[T - 32] = w[T & 15];
+  } else if constexpr (T >= 64) {
+    w[T & 15] = rotl(__builtin_amdgcn_bitop3_b32(p[T - 64], w[(T - 12) & 15], q[T - 64], 0x96), 4);
+  }
+  return w[T & 15];
+}
+
+template <int T>
+__device__ __forceinline__ void rounds_pair_from(uint32_t (&w)[16], uint32_t (&p)[16], uint32_t (&q)[16],
+                                                 uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e) {
+  if constexpr (T < 80) {
+    sha1_round<T>(a, b, c, d, e, sched_pair<T>(w, p, q));
+    rounds_pair_from<T + 1>(w, p, q, a, b, c, d, e);
+  }
+}
+
 // One compression of the 16 big-endian message words w (clobbered).
 __device__ __forceinline__ void compress(State &s, uint32_t (&w)[16]) {
   uint32_t a = s.h0, b = s.h1, c = s.h2, d = s.h3, e = s.h4;
-  rounds_from<0>(w, a, b, c, d, e);
+  uint32_t p[16], q[16];
+  rounds_pair_from<0>(w, p, q, a, b, c, d, e);
   s.h0 += a;  // sha.c:446-450
   s.h1 += b;
   s.h2 += c;

@@ -32,7 +32,7 @@ rocminfo 2>/dev/null | grep -m1 -E "gfx950" > "$OUT/device.txt" || true
 for step in "$@"; do
   case $step in
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run pytest_gpu 900 python3 -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    tests) run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     bench) run bench 600 python3 bench.py ;;
     bench_rings)
       for r in 2 3 4; do run bench_ring$r 300 python3 bench.py --ring $r --steps 10 --no-cpu-baseline; done ;;

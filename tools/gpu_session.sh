@@ -98,6 +98,13 @@ for step in "$@"; do
       sp=$!
       run power_stream 300 "$ROOT/tools/ubench/streamread" 400
       wait $sp ;;
+    variants597)
+      for rep in 1 2; do
+        for v in "3 1 0" "2 1 0" "4 1 0" "2 2 0" "10 1 0"; do
+          set -- $v
+          run "v597_$1$2$3_$rep" 300 python3 bench.py --ring $1 --lines $2 --nt $3 --steps 20 --no-cpu-baseline
+        done
+      done ;;
     lds_ab)
       for rep in 1 2; do
         run "ab_ring3_$rep" 300 python3 bench.py --ring 3 --steps 20 --no-cpu-baseline

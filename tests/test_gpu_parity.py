@@ -567,3 +567,28 @@ def test_peer_download_flow_end_to_end(bt, torch, tmp_path):
     v.close()
     assert failures == 1
     assert out.read_bytes() == img  # diff A.tar test1.tar
+
+
+def test_randomized_layouts_vs_oracle(bt, torch, oracle):
+    """Seeded random batches: chunk length, pitch, count, input offset (alignment)
+    and digest-output offset drawn at random, so both the hot kernel (aligned
+    layouts) and the generic kernel (anything else) see shapes no fixed case
+    names.  Every digest checked against the oracle."""
+    rng = random.Random(0xB17)
+    for case in range(40):
+        chunk_len = rng.choice([rng.randrange(0, 200), rng.randrange(0, 5000), rng.randrange(60000, 70000)])
+        pitch = chunk_len + rng.choice([0, 0, 16 - (chunk_len % 16 or 16), rng.randrange(0, 300)])
+        pitch = max(pitch, 1)
+        n = rng.choice([1, 2, 63, 64, 65, rng.randrange(1, 300)])
+        in_off = rng.choice([0, 0, 16, rng.randrange(0, 16)])
+        out_off = rng.choice([0, 0, 4, rng.randrange(0, 4)])
+        total = pitch * (n - 1) + chunk_len
+        host = bytearray(oracle.fill_synthetic(total + 16, case, 0xFEED))[:total]
+        d = to_dev(torch, bytes(in_off) + bytes(host), pad=16)
+        out = torch.zeros(20 * n + 8, dtype=torch.uint8, device="cuda")
+        bt.chunks_dev(d.data_ptr() + in_off, n, chunk_len, pitch, out.data_ptr() + out_off)
+        torch.cuda.synchronize()
+        raw = bytes(out.cpu().numpy().tobytes())[out_off:out_off + 20 * n]
+        for i in range(n):
+            want = oracle.sha1(bytes(host[i * pitch:i * pitch + chunk_len]))
+            assert raw[20 * i:20 * i + 20] == want, (case, chunk_len, pitch, n, in_off, out_off, i)

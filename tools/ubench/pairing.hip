@@ -22,6 +22,8 @@
 #define S1CH S(0) S(0) S(0) S(0) S(0) S(0) S(0) S(0)
 #define S2CH S(0) S(1) S(0) S(1) S(0) S(1) S(0) S(1)
 #define CB8 C(0) B(1) C(2) B(3) C(4) B(5) C(6) B(7)
+#define CCB8 C(0) C(1) B(2) C(3) C(4) B(5) C(6) C(7)
+#define CCCCB C(0) C(1) C(2) C(3) B(4)
 
 template <int M>
 __global__ __launch_bounds__(512) void kern(uint32_t *out, int iters) {
@@ -31,7 +33,7 @@ __global__ __launch_bounds__(512) void kern(uint32_t *out, int iters) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   bool s_wave;
   if constexpr (M == 0 || M == 5) s_wave = true;
-  else if constexpr (M == 13) s_wave = w < 4;
+  else if constexpr (M == 13 || M == 15 || M == 16) s_wave = w < 4;
   else if constexpr (M == 1) s_wave = false;
   else if constexpr (M == 2 || M == 6) s_wave = w < 4;
   else s_wave = (w & 1) == 0;
@@ -52,6 +54,16 @@ __global__ __launch_bounds__(512) void kern(uint32_t *out, int iters) {
       CB8 CB8 CB8
     } else if constexpr (M == 13) {
       if (s_wave) { CS8 CS8 CS8 } else { S(0) CS8 CS8 CS8 }  // SIMD partner offset by one
+    } else if constexpr (M == 14) {
+      C8 C8 S8                                               // 2:1, grouped runs
+    } else if constexpr (M == 15) {
+      if (s_wave) { CCS8 CCS8 CCS8 } else { C(7) CCS8 CCS8 C(0) C(1) S(2) C(3) C(4) S(5) C(6) }  // partner shifted by one
+    } else if constexpr (M == 16) {
+      if (s_wave) { C8 C8 S8 } else { S8 C8 C8 }             // grouped, partner in the other phase
+    } else if constexpr (M == 17) {
+      CCB8 CCB8 CCB8                                         // 2:1 with bitop3 as the full-rate op
+    } else if constexpr (M == 18) {
+      CCCCB CCCCB CCCCB CCCCB C(0) C(1) C(2) C(3)            // the round's 4:1 (24 instr)
     } else if constexpr (M == 5) {
       B8 B8 B8
     } else if constexpr (M == 6) {
@@ -100,5 +112,10 @@ int main() {
   run<11>("all xor, 2 chains");
   run<12>("all alternate add3,bitop3");
   run<13>("C,S alt; waves4-7 offset 1");
+  run<14>("C8 C8 S8 grouped (2:1)");
+  run<15>("C C S, partner offset 1");
+  run<16>("C8C8S8 vs S8C8C8 partner");
+  run<17>("C C bitop3 (2:1)");
+  run<18>("(C C C C bitop3) rounds 4:1");
   return 0;
 }

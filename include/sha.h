@@ -15,10 +15,8 @@
 
 #include <inttypes.h>
 
-#define SHA1_HASH_SIZE 20
-
-/* Hash size in 32-bit words */
-#define SHA1_HASH_WORDS 5
+#define SHA1_HASH_SIZE 20  /* digest bytes (sha.h:34)                     */
+#define SHA1_HASH_WORDS 5  /* digest as big-endian 32-bit words (sha.h:37) */
 
 struct _SHA1Context {
   uint64_t totalLength;             /* message bits absorbed so far      */

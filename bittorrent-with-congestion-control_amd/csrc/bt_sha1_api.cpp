@@ -501,7 +501,9 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
   return n;
 }
 
-// Single message on the GPU (shahash): stage, ragged kernel, 20 bytes back.
+// Single message on the GPU (shahash): stage into the aligned device buffer,
+// hash it as a one-chunk batch (the hot kernel's prefetching ring when the
+// message fits its 32-bit offsets, else the ragged kernel), 20 bytes back.
 int hash_one(DevCtx *c, const uint8_t *buf, uint32_t len, uint8_t out[20]) {
   if (ensure_streams(c)) return -1;
   if (c->h_msg.ensure((size_t)len + 64) || c->d_msg.ensure((size_t)len + 64) || c->d_state.ensure(64) ||
@@ -509,7 +511,7 @@ int hash_one(DevCtx *c, const uint8_t *buf, uint32_t len, uint8_t out[20]) {
     return -1;
   if (len) memcpy(c->h_msg.p, buf, len);
   if (len) BT_CK(hipMemcpyAsync(c->d_msg.p, c->h_msg.p, len, hipMemcpyHostToDevice, c->s));
-  BT_CK(btsha1_launch_ragged(c->d_msg.p, nullptr, nullptr, 0, len, 1, c->d_state.as<uint8_t>(), c->s));
+  if (launch_chunks(c->d_msg.p, 1, len, ((uint64_t)len + 15) & ~15ull, c->d_state.as<uint8_t>(), c->s)) return -1;
   BT_CK(hipMemcpyAsync(c->h_state.p, c->d_state.p, 20, hipMemcpyDeviceToHost, c->s));
   BT_CK(hipStreamSynchronize(c->s));
   memcpy(out, c->h_state.p, 20);

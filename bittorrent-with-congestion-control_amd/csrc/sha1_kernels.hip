@@ -256,29 +256,57 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
 // ---------------------------------------------------------------------------
 // Generic paths (64-bit addressing, any alignment).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t load_be_word(const uint8_t *p, uint32_t align) {
-  if (align == 0) return bswap(*(const uint32_t *)p);
-  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
-}
-
-__device__ __forceinline__ void absorb_blocks(State &st, const uint8_t *p, uint64_t nblocks) {
-  const uint32_t align = (uint32_t)((uintptr_t)p & 15u);
-  if (align == 0) {
-    const u32x4 *q = (const u32x4 *)p;
-    for (uint64_t b = 0; b < nblocks; ++b, q += 4) {
-      uint32_t w[16];
-      block_from_le(w, q[0], q[1], q[2], q[3]);
-      compress(st, w);
-    }
-  } else {
-    const uint32_t a4 = (uint32_t)((uintptr_t)p & 3u);
-    for (uint64_t b = 0; b < nblocks; ++b, p += 64) {
-      uint32_t w[16];
+// Block source for absorb_ring: how one 64-byte block is fetched into a
+// register slot and turned into 16 big-endian words (sha.c:186-189).  The
+// loads are 16-byte loads at the message's own alignment: gfx950 under HSA
+// runs in unaligned-access mode (hipcc emits global_load_dwordx4 for an
+// unaligned memcpy), so a byte-misaligned message costs four loads per block
+// like an aligned one, instead of one load per byte or word.
+struct SrcBytes {
+  typedef u32x4 Slot[4];
+  const uint8_t *p;
+  __device__ __forceinline__ void load(Slot &s, uint64_t k) const {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) w[j] = load_be_word(p + 4 * j, a4);
+    for (int i = 0; i < 4; ++i) __builtin_memcpy(&s[i], p + 64 * k + 16 * i, 16);
+  }
+  __device__ __forceinline__ void words(uint32_t (&w)[16], const Slot &s) const { block_from_le(w, s[0], s[1], s[2], s[3]); }
+};
+
+// Whole blocks through a 3-slot register ring: block k+2 is fetched while
+// block k is compressed, so a lone chain (shahash, a ragged message, the
+// streaming API) does not wait on memory once per block.  Prefetches are
+// guarded per lane (k+2 < nblocks): nothing past the message is read.
+template <class Src>
+__device__ __forceinline__ void absorb_ring(State &st, const Src &src, uint64_t nblocks) {
+  typename Src::Slot ring[3];
+  if (nblocks > 0) src.load(ring[0], 0);
+  if (nblocks > 1) src.load(ring[1], 1);
+  uint64_t k = 0;
+  for (; k + 3 <= nblocks; k += 3) {
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      if (k + s + 2 < nblocks) src.load(ring[(s + 2) % 3], k + s + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t w[16];
+      src.words(w, ring[s]);
       compress(st, w);
     }
   }
+  // 0..2 blocks left; they are already in ring[0], ring[1].
+  if (k < nblocks) {
+    uint32_t w[16];
+    src.words(w, ring[0]);
+    compress(st, w);
+  }
+  if (k + 1 < nblocks) {
+    uint32_t w[16];
+    src.words(w, ring[1]);
+    compress(st, w);
+  }
+}
+
+__device__ __forceinline__ void absorb_blocks(State &st, const uint8_t *p, uint64_t nblocks) {
+  absorb_ring(st, SrcBytes{p}, nblocks);
 }
 
 __device__ __forceinline__ void absorb_tail_and_finish(State &st, const uint8_t *p, uint32_t r, uint64_t len) {
@@ -301,7 +329,7 @@ __global__ __launch_bounds__(kBlock) void k_sha1_ragged(const uint8_t *__restric
                                                         const uint32_t *__restrict__ lens, uint64_t pitch,
                                                         uint32_t fixed_len, uint64_t n,
                                                         uint8_t *__restrict__ digests) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t *p = base + (offsets ? offsets[i] : i * pitch);
   const uint32_t len = offsets ? lens[i] : fixed_len;
@@ -486,8 +514,11 @@ hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uin
 hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t pitch,
                                 uint32_t fixed_len, uint64_t n, uint8_t *d_dig, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t grid = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_sha1_ragged, dim3((uint32_t)grid), dim3(kBlock), 0, s, (const uint8_t *)d_base, d_off,
+  // As launch_fixed_v: below one wave per SIMD, one-wave workgroups spread
+  // the chains over CUs (each message is a serial chain).
+  const uint32_t wg = n < 65536 ? 64u : (uint32_t)kBlock;
+  const uint64_t grid = (n + wg - 1) / wg;
+  hipLaunchKernelGGL(k_sha1_ragged, dim3((uint32_t)grid), dim3(wg), 0, s, (const uint8_t *)d_base, d_off,
                      d_len, pitch, fixed_len, n, d_dig);
   return hipGetLastError();
 }

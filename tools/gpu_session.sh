@@ -161,6 +161,7 @@ for step in "$@"; do
       mkdir -p "$OUT/stream_prof"
       run stream_prof 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/stream_prof" -o sb \
         -- python3 "$ROOT/tools/stream_bench.py" 4 ;;
+    latency) run latency 300 python3 tools/latency_bench.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

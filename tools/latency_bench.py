@@ -1,0 +1,139 @@
+#!/usr/bin/env python3
+"""tools/latency_bench.py -- latency of the single-message and ragged paths.
+
+The hot kernel is throughput-shaped (131072 chunks in flight).  The drop-in
+callers that keep the reference's synchronous contract pay a chunk's serial
+chain instead: util.c:311 calls shahash once per received chunk, and
+make_chunks hashes its short last chunk alone (chunk.c:20-21).  This prints
+one JSON line per measurement (median of --reps):
+
+  shahash_512k      shahash() of one 512 KiB host buffer, call to return
+  ragged_1x512k     bt_sha1_ragged_dev over one device-resident 512 KiB message
+  ragged_1x512k_u   the same message at an odd byte offset (unaligned loads)
+  ragged_4096       4096 device-resident messages of 480-544 KiB at 16-byte
+                    aligned offsets (GiB/s of message bytes)
+  ragged_4096_u     the same lengths at arbitrary byte offsets
+  update_1484       SHA1Update of one 512 KiB chunk fed as 1484-byte payloads
+                    (save_data_packet's granule, util.c:275) + SHA1Final
+  verifier_b1       bt_sha1_verifier with batch 1: submit -> verdict
+Digests are checked against the oracle (hashlib is not used).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "bittorrent-with-congestion-control_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+CHUNK = 512 * 1024
+
+
+def emit(name, samples_s, extra=None):
+    med = statistics.median(samples_s)
+    d = {"case": name, "median_ms": round(med * 1e3, 4), "min_ms": round(min(samples_s) * 1e3, 4),
+         "reps": len(samples_s)}
+    d.update(extra or {})
+    print(json.dumps(d), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=9)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import btsha1 as bt
+    import py_oracle as orc
+
+    rng = np.random.default_rng(7)
+    msg = bytes(orc.fill_synthetic(CHUNK, 0, orc.SEED_SYNTH))
+    want = orc.sha1(msg)
+
+    # shahash: host buffer in, 20 bytes out, synchronous (chunk.c:33-49).
+    assert bt.shahash(msg) == want
+    ts = []
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        got = bt.shahash(msg)
+        ts.append(time.perf_counter() - t0)
+    assert got == want
+    emit("shahash_512k", ts)
+
+    s = torch.cuda.Stream()  # a real stream: handle 0 would mean "library stream" to the C-ABI
+    torch.cuda.set_stream(s)
+    dev = torch.empty(CHUNK + 4096, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(20 * 4096, dtype=torch.uint8, device="cuda")
+
+    def ragged(base, offs, lens):
+        o = torch.tensor(offs, dtype=torch.int64, device="cuda")
+        ln = torch.tensor(lens, dtype=torch.int32, device="cuda")
+        res = []
+        for _ in range(args.reps + 1):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            bt.ragged_dev(base, o.data_ptr(), ln.data_ptr(), len(offs), out.data_ptr(), s.cuda_stream)
+            b.record(s)
+            torch.cuda.synchronize()
+            res.append(a.elapsed_time(b) * 1e-3)
+        return res[1:]
+
+    for name, off in (("ragged_1x512k", 0), ("ragged_1x512k_u", 3)):
+        dev[off:off + CHUNK].copy_(torch.frombuffer(bytearray(msg), dtype=torch.uint8))
+        ts = ragged(dev.data_ptr(), [off], [CHUNK])
+        assert bytes(out[:20].cpu().numpy().tobytes()) == want, name
+        emit(name, ts, {"kernel": "k_sha1_ragged"})
+
+    n = 4096
+    lens = [int(x) for x in rng.integers(480 * 1024, 544 * 1024, n)]
+    for name, aligned in (("ragged_4096", True), ("ragged_4096_u", False)):
+        offs, pos = [], 0
+        for ln in lens:
+            pos += int(rng.integers(0, 16)) if not aligned else 0
+            offs.append(pos)
+            pos += ln
+            pos = (pos + 15) & ~15 if aligned else pos
+        total = pos + 64
+        big = torch.empty(total, dtype=torch.uint8, device="cuda")
+        bt.fill_synthetic(big.data_ptr(), total, 12345, orc.SEED_SYNTH, s.cuda_stream)
+        torch.cuda.synchronize()
+        ts = ragged(big.data_ptr(), offs, lens)
+        host = big.cpu().numpy()
+        for i in list(range(0, n, 511)) + [n - 1]:
+            assert bytes(out[20 * i:20 * i + 20].cpu().numpy().tobytes()) == \
+                orc.sha1(host[offs[i]:offs[i] + lens[i]].tobytes()), (name, i)
+        med = statistics.median(ts)
+        emit(name, ts, {"kernel": "k_sha1_ragged", "messages": n,
+                        "GiB_per_s": round(sum(lens) / med / 2**30, 2)})
+        del big
+
+    # Streaming API at the peer's packet granule.
+    ts = []
+    for _ in range(max(1, args.reps // 3)):
+        t0 = time.perf_counter()
+        h = bt.Sha1()
+        for o in range(0, CHUNK, 1484):
+            h.update(msg[o:o + 1484])
+        got = h.final()
+        ts.append(time.perf_counter() - t0)
+    assert got == want
+    emit("update_1484", ts)
+
+    v = bt.Verifier(batch=1, nstreams=2)
+    ts = []
+    for i in range(args.reps):
+        t0 = time.perf_counter()
+        v.submit(msg, want, tag=i)
+        r = v.drain()
+        ts.append(time.perf_counter() - t0)
+        assert r == [(i, True, want)], r
+    v.close()
+    emit("verifier_b1", ts)
+
+
+if __name__ == "__main__":
+    main()

@@ -191,10 +191,16 @@ int launch_chunks(const void *d_in, uint64_t n, uint64_t len, uint64_t pitch, ui
   return 0;
 }
 
-// A contiguous host image: full chunks through the hot kernel, a short last
-// chunk (make_chunks' final fread, chunk.c:20) through the ragged kernel.
+// A contiguous image: full chunks through the hot kernel, a short last chunk
+// (make_chunks' final fread, chunk.c:20) in the same launch as its tail wave
+// when the layout allows, else through the ragged kernel after it.
 int launch_image(const uint8_t *d_img, uint64_t bytes, uint64_t chunk_len, uint8_t *d_dig, hipStream_t s) {
   const uint64_t nfull = bytes / chunk_len, rem = bytes % chunk_len;
+  if (fast_layout(d_img, chunk_len, chunk_len, d_dig)) {
+    BT_CK(btsha1_launch_fixed(d_img, nfull, (uint32_t)chunk_len, (uint32_t)chunk_len, d_dig, nullptr, nullptr, s,
+                              g_variant.load(), (uint32_t)rem));
+    return 0;
+  }
   if (launch_chunks(d_img, nfull, chunk_len, chunk_len, d_dig, s)) return -1;
   if (rem) BT_CK(btsha1_launch_ragged(d_img + nfull * chunk_len, nullptr, nullptr, 0, (uint32_t)rem, 1,
                                       d_dig + 20 * nfull, s));

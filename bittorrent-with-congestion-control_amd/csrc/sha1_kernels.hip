@@ -101,16 +101,27 @@ __device__ __forceinline__ void epilogue(State &st, __amdgpu_buffer_rsrc_t rsrc,
 }
 
 // NBUF ring slots of L lines; AUX = buffer-load cache policy (0 default, 2 nt).
+// tail_len != 0: one more, shorter chunk follows the n_chunks full ones (the
+// last fread of make_chunks, chunk.c:20); the first wave past the full ones
+// (chunk0 = n_chunks rounded up to 64) hashes it alone, inside the same launch,
+// so its chain runs beside the full chunks' instead of after them.
 template <int NBUF, int L, int AUX, bool VERIFY>
 __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sha1_fixed(
     const uint8_t *__restrict__ base, uint64_t n_chunks, uint32_t pitch, uint32_t len, uint8_t *__restrict__ digests,
-    const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok) {
+    const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok, uint32_t tail_len) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t chunk0 = (uint64_t)blockIdx.x * blockDim.x + (uint64_t)wave * 64u;  // wave-uniform
-  if (chunk0 >= n_chunks) return;
-  const uint64_t left = n_chunks - chunk0;
-  const uint32_t nvalid = left < 64 ? (uint32_t)left : 64u;
+  uint64_t chunk0 = (uint64_t)blockIdx.x * blockDim.x + (uint64_t)wave * 64u;  // wave-uniform
+  uint32_t nvalid;
+  if (chunk0 < n_chunks) {
+    const uint64_t left = n_chunks - chunk0;
+    nvalid = left < 64 ? (uint32_t)left : 64u;
+  } else {
+    if (tail_len == 0 || chunk0 != ((n_chunks + 63u) & ~(uint64_t)63u)) return;
+    chunk0 = n_chunks;  // the tail chunk: digest index n_chunks, bytes at n_chunks * pitch
+    nvalid = 1;
+    len = tail_len;
+  }
   // Lanes past the end re-hash the wave's last chunk (no divergence, no store).
   const uint32_t mine = lane < nvalid ? lane : nvalid - 1u;
   const uint32_t voff = mine * pitch;
@@ -456,19 +467,20 @@ using namespace btsha1;
 
 template <int NBUF, int L, int AUX>
 static hipError_t launch_fixed_v(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
-                                 const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s) {
+                                 const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, uint32_t tail_len) {
   // Below one wave per SIMD (256 CUs x 4 SIMDs x 64 lanes) use one-wave
   // workgroups so the dispatcher spreads the waves over distinct CUs instead
   // of stacking four per CU: a chunk's latency is its serial 8193-block chain,
   // so a lone wave per SIMD finishes the batch soonest.
   const uint32_t wg = n < 65536 ? 64u : (uint32_t)kBlock;
-  const uint64_t grid = (n + wg - 1) / wg;
+  const uint64_t threads = tail_len ? ((n + 63) & ~(uint64_t)63) + 64 : n;  // + the tail wave
+  const uint64_t grid = (threads + wg - 1) / wg;
   if (d_ok)
     hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, true>), dim3((uint32_t)grid), dim3(wg), 0, s,
-                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok);
+                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok, tail_len);
   else
     hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, false>), dim3((uint32_t)grid), dim3(wg), 0, s,
-                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok);
+                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok, tail_len);
   return hipGetLastError();
 }
 
@@ -500,12 +512,23 @@ bool btsha1_fixed_variant_ok(int code) {
 }
 
 hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
-                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant) {
-  if (n == 0) return hipSuccess;
-  if (variant == kLdsVariant) return launch_lds<0>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
-  if (variant == kLdsNtVariant) return launch_lds<2>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
+                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant, uint32_t tail_len) {
+  if (tail_len && d_ok) return hipErrorInvalidValue;  // verify batches are whole chunks
+  if (n == 0 && tail_len == 0) return hipSuccess;
+  if (variant == kLdsVariant || variant == kLdsNtVariant) {
+    if (n) {
+      const hipError_t e = variant == kLdsVariant ? launch_lds<0>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s)
+                                                  : launch_lds<2>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
+      if (e != hipSuccess) return e;
+    }
+    // The LDS-staged variant has no tail wave: the tail follows on the stream.
+    return tail_len ? btsha1_launch_ragged((const uint8_t *)d_in + n * (uint64_t)pitch, nullptr, nullptr, 0, tail_len, 1,
+                                           d_dig ? d_dig + 20 * n : nullptr, s)
+                    : hipSuccess;
+  }
 #define BT_CASE(N, L, A) \
-  if (variant == N * 100 + L * 10 + (A ? 1 : 0)) return launch_fixed_v<N, L, A>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s);
+  if (variant == N * 100 + L * 10 + (A ? 1 : 0)) \
+    return launch_fixed_v<N, L, A>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s, tail_len);
   BT_FIXED_VARIANTS(BT_CASE)
 #undef BT_CASE
   return hipErrorInvalidValue;

@@ -7,8 +7,11 @@
 // n equal chunks of `len` bytes at `pitch` (16-byte multiple, 64*pitch < 4 GiB),
 // d_in 16-byte aligned.  d_dig: 20*n bytes (4-byte aligned) or NULL.  When
 // d_ok != NULL also compares against d_exp (20*n) and writes one byte per chunk.
+// tail_len (0 < tail_len < len, no d_ok): one more chunk of tail_len bytes at
+// d_in + n*pitch, digest at d_dig + 20*n, hashed in the same launch.
 hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
-                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant);
+                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant,
+                               uint32_t tail_len = 0);
 // Hot-kernel variant code = ring slots*100 + lines per slot*10 + nt flag.
 bool btsha1_fixed_variant_ok(int code);
 // n messages at d_base + d_off[i], d_len[i] bytes each; with d_off == NULL,

@@ -227,6 +227,22 @@ def test_host_pipeline_c_tar_and_tail(bt, oracle):
     assert bt.chunks_host(big, chunk_len=4096) == oracle.hash_chunks(big, 4096)
 
 
+@pytest.mark.parametrize("variant", [(3, 1, 0), (2, 2, 0), (LDS, 1, 0)])
+def test_image_tail_in_same_launch(bt, oracle, variant):
+    """launch_image: the short last chunk rides in the hot kernel's tail wave
+    (the LDS-staged variant hands it to the ragged kernel instead)."""
+    bt.set_variant(*variant)
+    try:
+        for chunk_len in (4096, 64 * 1024):
+            for nfull in (0, 1, 63, 64, 65, 130):
+                for rem in (1, 3, 55, 56, 63, 64, 65, 1000, chunk_len - 1):
+                    img = bytes(oracle.fill_synthetic(nfull * chunk_len + rem, nfull + rem, 0x7A11))
+                    assert bt.chunks_host(img, chunk_len=chunk_len) == oracle.hash_chunks(img, chunk_len), \
+                        (variant, chunk_len, nfull, rem)
+    finally:
+        bt.set_variant(3, 1, 0)
+
+
 def test_make_chunks_file_api(bt, oracle, tmp_path):
     p = tmp_path / "C.tar"
     p.write_bytes(c_tar_bytes())

@@ -31,7 +31,7 @@ def compile_asm(out):
 
 
 def loop_mix(asm_text, nbuf, lines):
-    sym = f"_ZN6btsha112k_sha1_fixedILi{nbuf}ELi{lines}ELi0ELb0EEEvPKhmjjPhS2_S3_"
+    sym = f"_ZN6btsha112k_sha1_fixedILi{nbuf}ELi{lines}ELi0ELb0EEEvPKhmjjPhS2_S3_j"
     start = asm_text.index(sym + ":")
     body = asm_text[start:]
     end_fn = body.index(".Lfunc_end")

@@ -285,18 +285,24 @@ struct SrcBytes {
 
 // Whole blocks through a 3-slot register ring: block k+2 is fetched while
 // block k is compressed, so a lone chain (shahash, a ragged message, the
-// streaming API) does not wait on memory once per block.  Prefetches are
-// guarded per lane (k+2 < nblocks): nothing past the message is read.
+// streaming API) does not wait on memory once per block.  Prefetch indices
+// are clamped to the message's last block (re-read, never used) rather than
+// branched around: a load inside a branch makes the compiler wait for every
+// outstanding load at the join (vmcnt(0), seen in the ISA), which turns the
+// ring back into one memory round trip per block.
 template <class Src>
 __device__ __forceinline__ void absorb_ring(State &st, const Src &src, uint64_t nblocks) {
+  if (nblocks == 0) return;
+  const uint64_t last = nblocks - 1;
   typename Src::Slot ring[3];
-  if (nblocks > 0) src.load(ring[0], 0);
-  if (nblocks > 1) src.load(ring[1], 1);
+  src.load(ring[0], 0);
+  src.load(ring[1], last < 1 ? last : 1);
   uint64_t k = 0;
   for (; k + 3 <= nblocks; k += 3) {
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
-      if (k + s + 2 < nblocks) src.load(ring[(s + 2) % 3], k + s + 2);
+      const uint64_t nx = k + s + 2;
+      src.load(ring[(s + 2) % 3], nx < last ? nx : last);
       __builtin_amdgcn_sched_barrier(0);
       uint32_t w[16];
       src.words(w, ring[s]);

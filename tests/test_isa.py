@@ -54,3 +54,35 @@ def test_schedule_squared_twice_identity():
             assert w[t] == _rotl(w[t - 6] ^ w[t - 16] ^ w[t - 28] ^ w[t - 32], 2)
         for t in range(64, 80):
             assert w[t] == _rotl(w[t - 12] ^ w[t - 32] ^ w[t - 56] ^ w[t - 64], 4)
+
+
+def _first_wait_after_each_load_group(text, sym):
+    """For every run of 16-byte global loads in kernel `sym`, the vmcnt of the
+    first s_waitcnt that follows it."""
+    import re
+    body = text[text.index(sym + ":"):]
+    body = body[:body.index(".Lfunc_end")]
+    out, in_group = [], False
+    for line in body.splitlines():
+        line = line.strip()
+        if line.startswith("global_load_dwordx4"):
+            in_group = True
+            continue
+        m = re.match(r"s_waitcnt vmcnt\((\d+)\)", line)
+        if m and in_group:
+            out.append(int(m.group(1)))
+            in_group = False
+    return out
+
+
+@pytest.mark.parametrize("sym", ["_ZN6btsha113k_sha1_raggedEPKhPKmPKjmjmPh", "_ZN6btsha115k_sha1_midstateEPjPKhm"])
+def test_ragged_ring_keeps_loads_in_flight(asm, sym):
+    """The generic kernels' prefetch ring (absorb_ring) must not wait for the
+    block it just asked for: the first wait after each group of four 16-byte
+    loads leaves that whole group outstanding (vmcnt >= 4).  A guarded
+    (branched) prefetch made hipcc wait vmcnt(3..0) right after issuing it --
+    one memory round trip per block."""
+    _, text = asm
+    waits = _first_wait_after_each_load_group(text, sym)
+    assert waits, "no 16-byte load groups found"
+    assert min(waits) >= 4, waits

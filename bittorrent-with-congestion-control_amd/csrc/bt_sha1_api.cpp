@@ -65,6 +65,22 @@ void set_err(const char *fmt, ...) {
   abort();
 }
 
+// Entry points that must switch devices (host pipelines, drop-in calls, the
+// verifier) give the caller's thread its current device back on return, so
+// a caller that drives its own HIP work (torch on cuda:N) is not moved.
+struct KeepDevice {
+  int prev = -1;
+  KeepDevice() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~KeepDevice() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+  KeepDevice(const KeepDevice &) = delete;
+  KeepDevice &operator=(const KeepDevice &) = delete;
+};
+
 // Grow-only device / pinned scratch.
 struct DevBuf {
   void *p = nullptr;
@@ -142,6 +158,7 @@ DevCtx *ctx_for(int dev) {
   if (!g_ctx[dev]) {
     auto c = std::make_unique<DevCtx>();
     c->dev = dev;
+    KeepDevice keep_dev;
     if (hipSetDevice(dev) != hipSuccess) {
       set_err("cannot initialise HIP device %d", dev);
       return nullptr;
@@ -428,6 +445,7 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
 }
 
 int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t chunk_len, uint8_t *h_dig) {
+  KeepDevice keep_dev;
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
   std::lock_guard<std::mutex> g(c->mu);
@@ -455,6 +473,7 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
 
 template <class Sink>
 int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
+  KeepDevice keep_dev;
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
   std::lock_guard<std::mutex> g(c->mu);
@@ -800,6 +819,7 @@ void shahash(uint8_t *str, int len, uint8_t *hash) {
     set_err("negative length %d", len);
     die("shahash");
   }
+  KeepDevice keep_dev;
   DevCtx *c = dropin_ctx("shahash");
   std::lock_guard<std::mutex> g(c->mu);
   if (hash_one(c, str, (uint32_t)len, hash)) die("shahash");
@@ -856,6 +876,7 @@ void SHA1Update(SHA1Context *sc, const void *vdata, uint32_t len) {
   const uint64_t nfull = len / 64u;
   const bool staged_full = sc->bufferLength == 64u;
   if (staged_full || nfull) {
+    KeepDevice keep_dev;
     DevCtx *c = dropin_ctx("SHA1Update");
     std::lock_guard<std::mutex> g(c->mu);
     std::vector<uint8_t> tmp;
@@ -891,6 +912,7 @@ void SHA1Final(SHA1Context *sc, uint8_t hash[SHA1_HASH_SIZE]) {
   const uint64_t bits = sc->totalLength;
   const uint32_t end = bl + npad + 8u;  // 64 or 128
   for (int i = 0; i < 8; ++i) blk[end - 8 + i] = (uint8_t)(bits >> (56 - 8 * i));
+  KeepDevice keep_dev;
   DevCtx *c = dropin_ctx("SHA1Final");
   {
     std::lock_guard<std::mutex> g(c->mu);
@@ -1027,6 +1049,7 @@ bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32
     return nullptr;
   }
   if (!ctx_for(device)) return nullptr;
+  KeepDevice keep_dev;
   if (hipSetDevice(device) != hipSuccess) {
     set_err("hipSetDevice(%d) failed", device);
     return nullptr;
@@ -1057,6 +1080,7 @@ bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32
 
 void bt_sha1_verifier_destroy(bt_sha1_verifier *v) {
   if (!v) return;
+  KeepDevice keep_dev;
   (void)hipSetDevice(v->dev);
   for (auto &b : v->b) {
     if (b.s) (void)hipStreamSynchronize(b.s);
@@ -1073,6 +1097,7 @@ void bt_sha1_verifier_destroy(bt_sha1_verifier *v) {
 
 uint8_t *bt_sha1_verifier_slot(bt_sha1_verifier *v) {
   if (!v) return nullptr;
+  KeepDevice keep_dev;
   if (hipSetDevice(v->dev) != hipSuccess) return nullptr;
   if (v->b[v->fill].closed && v_advance(v)) return nullptr;
   VBatch &b = v->b[v->fill];
@@ -1092,6 +1117,7 @@ int bt_sha1_verifier_commit(bt_sha1_verifier *v, uint8_t *slot, uint32_t len, co
     set_err("verifier: chunk of %u bytes, verifier built for %u", len, v->chunk_len);
     return -1;
   }
+  KeepDevice keep_dev;
   if (hipSetDevice(v->dev) != hipSuccess) return -1;
   uint32_t bi, si;
   if (v_locate(v, slot, &bi, &si)) return -1;
@@ -1109,6 +1135,7 @@ int bt_sha1_verifier_release(bt_sha1_verifier *v, uint8_t *slot) {
     set_err("null pointer");
     return -1;
   }
+  KeepDevice keep_dev;
   if (hipSetDevice(v->dev) != hipSuccess) return -1;
   uint32_t bi, si;
   if (v_locate(v, slot, &bi, &si)) return -1;
@@ -1137,6 +1164,7 @@ int bt_sha1_verifier_submit(bt_sha1_verifier *v, const void *h_chunk, uint32_t l
 
 int bt_sha1_verifier_flush(bt_sha1_verifier *v) {
   if (!v) return -1;
+  KeepDevice keep_dev;
   if (hipSetDevice(v->dev) != hipSuccess) return -1;
   VBatch &b = v->b[v->fill];
   if (b.reserved == 0 || b.closed) return 0;
@@ -1156,6 +1184,7 @@ static int v_take(bt_sha1_verifier *v, bt_sha1_verdict *out, int max) {
 
 int bt_sha1_verifier_poll(bt_sha1_verifier *v, bt_sha1_verdict *out, int max) {
   if (!v) return -1;
+  KeepDevice keep_dev;
   if (hipSetDevice(v->dev) != hipSuccess) return -1;
   while (!v->order.empty()) {
     VBatch &b = v->b[v->order.front()];

@@ -53,6 +53,19 @@ def test_shahash_kats(bt):
         assert bt.shahash(data[name]).hex() == h, name
 
 
+def test_shahash_either_side_of_the_hot_kernel_limit(bt, oracle):
+    """shahash takes the hot kernel while 64*pitch + 4096 fits 32-bit buffer
+    offsets (messages up to ~64 MiB) and the ragged kernel past it; both
+    sides of the limit, plus short messages at every residue mod 64."""
+    limit = ((1 << 32) - 4096) // 64  # largest 16-byte pitch the hot kernel takes
+    for n in (limit - 16 - 7, limit + 1):
+        msg = bytes(oracle.fill_synthetic(n, n, 0x51A7))
+        assert bt.shahash(msg) == oracle.sha1(msg), n
+    base = bytes(oracle.fill_synthetic(200, 1, 0x51A7))
+    for n in range(0, 200):
+        assert bt.shahash(base[:n]) == oracle.sha1(base[:n]), n
+
+
 def test_streaming_api_kats_random_splits(bt):
     data = kat_data()
     rng = random.Random(1)

@@ -53,6 +53,7 @@ _sig("bt_sha1_last_error", ctypes.c_char_p)
 _sig("bt_sha1_build_info", ctypes.c_char_p)
 _sig("bt_sha1_set_ring_depth", ctypes.c_int, ctypes.c_int)
 _sig("bt_sha1_set_variant", ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int)
+_sig("bt_sha1_set_latency_batch", _u64, _u64)
 _sig("bt_sha1_chunks_dev", ctypes.c_int, _vp, _u64, _u64, _u64, _vp, _vp)
 _sig("bt_sha1_verify_dev", ctypes.c_int, _vp, _u64, _u64, _u64, _vp, _vp, _vp, _vp)
 _sig("bt_sha1_ragged_dev", ctypes.c_int, _vp, _vp, _vp, _u64, _vp, _vp)
@@ -114,6 +115,11 @@ def set_ring_depth(nbuf):
 
 def set_variant(nbuf, lines=1, nt=0):
     _check(lib.bt_sha1_set_variant(nbuf, lines, nt), "set_variant")
+
+
+def set_latency_batch(max_chunks):
+    """Batches of <= max_chunks take the latency kernel (0: never); returns the previous value."""
+    return lib.bt_sha1_set_latency_batch(max_chunks)
 
 
 def build_info():

@@ -593,12 +593,18 @@ const char *bt_sha1_last_error(void) { return t_err.c_str(); }
 
 const char *bt_sha1_build_info(void) {
   static char info[128];
-  snprintf(info, sizeof info, "libbtsha1 gfx950 hip%d.%d ring=%d", HIP_VERSION_MAJOR, HIP_VERSION_MINOR,
-           g_variant.load());
+  snprintf(info, sizeof info, "libbtsha1 gfx950 hip%d.%d ring=%d latency_batch=%llu", HIP_VERSION_MAJOR,
+           HIP_VERSION_MINOR, g_variant.load(), (unsigned long long)btsha1_latency_batch());
   return info;
 }
 
 int bt_sha1_set_ring_depth(int nbuf) { return bt_sha1_set_variant(nbuf, 1, 0); }
+
+uint64_t bt_sha1_set_latency_batch(uint64_t max_chunks) {
+  const uint64_t prev = btsha1_latency_batch();
+  btsha1_set_latency_batch(max_chunks);
+  return prev;
+}
 
 int bt_sha1_set_variant(int nbuf, int lines, int nt) {
   const int code = nbuf * 100 + lines * 10 + (nt ? 1 : 0);

@@ -51,6 +51,44 @@ __device__ __forceinline__ void compress_slot(State &st, const u32x4 (&q)[8 * L]
   }
 }
 
+// The r = len % 64 trailing bytes of the lane's chunk as big-endian words,
+// bytes past r zero (4-byte buffer loads, range-checked).
+__device__ __forceinline__ void load_tail(uint32_t (&tail)[16], __amdgpu_buffer_rsrc_t rsrc, uint32_t voff,
+                                          uint32_t nblocks, uint32_t r) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t have = r > 4u * j ? r - 4u * j : 0u;
+    uint32_t v = 0;
+    if (have) v = keep_be_bytes(bswap(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, nblocks * 64u + 4u * j, 0)), have);
+    tail[j] = v;
+  }
+}
+
+// Digest store (sha.c:550-553 big-endian bytes) and the optional fused
+// compare of util.c:311-313, for the lanes that own a chunk.
+template <bool VERIFY>
+__device__ __forceinline__ void store_digest(const State &st, uint32_t lane, uint32_t nvalid, uint64_t chunk0,
+                                             uint8_t *__restrict__ digests, const uint8_t *__restrict__ expected,
+                                             uint8_t *__restrict__ ok) {
+  if (lane < nvalid) {
+    const uint64_t idx = chunk0 + lane;
+    const uint32_t d0 = bswap(st.h0), d1 = bswap(st.h1), d2 = bswap(st.h2), d3 = bswap(st.h3), d4 = bswap(st.h4);
+    if (digests) {
+      uint32_t *o = (uint32_t *)(digests + idx * 20u);
+      o[0] = d0; o[1] = d1; o[2] = d2; o[3] = d3; o[4] = d4;
+    }
+    if constexpr (VERIFY) {  // memcmp(hash, chunk->hash, 20) == 0
+      const uint8_t *x = expected + idx * 20u;
+      uint32_t e[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        e[k] = (uint32_t)x[4 * k] | ((uint32_t)x[4 * k + 1] << 8) | ((uint32_t)x[4 * k + 2] << 16) |
+               ((uint32_t)x[4 * k + 3] << 24);
+      ok[idx] = (uint8_t)((e[0] == d0) & (e[1] == d1) & (e[2] == d2) & (e[3] == d3) & (e[4] == d4));
+    }
+  }
+}
+
 // Shared tail of the fixed-layout kernels: whole blocks from `done` on (fewer
 // than one ring turn), the tail bytes + MD padding, the digest store and the
 // optional fused compare.
@@ -72,32 +110,9 @@ __device__ __forceinline__ void epilogue(State &st, __amdgpu_buffer_rsrc_t rsrc,
   // Tail bytes + MD padding (sha.c:536-543); r is uniform across the batch.
   const uint32_t r = len & 63u;
   uint32_t tail[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t have = r > 4u * j ? r - 4u * j : 0u;
-    uint32_t v = 0;
-    if (have) v = keep_be_bytes(bswap(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, nblocks * 64u + 4u * j, 0)), have);
-    tail[j] = v;
-  }
+  load_tail(tail, rsrc, voff, nblocks, r);
   finish(st, tail, r, len);
-
-  if (lane < nvalid) {
-    const uint64_t idx = chunk0 + lane;
-    const uint32_t d0 = bswap(st.h0), d1 = bswap(st.h1), d2 = bswap(st.h2), d3 = bswap(st.h3), d4 = bswap(st.h4);
-    if (digests) {
-      uint32_t *o = (uint32_t *)(digests + idx * 20u);  // sha.c:550-553 big-endian bytes
-      o[0] = d0; o[1] = d1; o[2] = d2; o[3] = d3; o[4] = d4;
-    }
-    if constexpr (VERIFY) {  // util.c:311-313: memcmp(hash, chunk->hash, 20) == 0
-      const uint8_t *x = expected + idx * 20u;
-      uint32_t e[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k)
-        e[k] = (uint32_t)x[4 * k] | ((uint32_t)x[4 * k + 1] << 8) | ((uint32_t)x[4 * k + 2] << 16) |
-               ((uint32_t)x[4 * k + 3] << 24);
-      ok[idx] = (uint8_t)((e[0] == d0) & (e[1] == d1) & (e[2] == d2) & (e[3] == d3) & (e[4] == d4));
-    }
-  }
+  store_digest<VERIFY>(st, lane, nvalid, chunk0, digests, expected, ok);
 }
 
 // NBUF ring slots of L lines; AUX = buffer-load cache policy (0 default, 2 nt).
@@ -262,6 +277,166 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
     }
   }
   epilogue<VERIFY>(st, rsrc, voff, nslots * 2u, len, lane, nvalid, chunk0, digests, expected, ok);
+}
+
+// ---------------------------------------------------------------------------
+// Latency kernel: small batches, where a chunk's latency is its serial chain.
+// ---------------------------------------------------------------------------
+// Below one wave per SIMD most SIMDs idle, and a lone wave issues at most one
+// instruction per ~4 cycles (tools/latency_bench.py), so a chain costs its
+// instruction count (8193 x 597 -> ~9 ms per 512 KiB).  Here every 64 chunks
+// get a workgroup of two waves on two SIMDs of one CU:
+//   wave S loads the message, byte-swaps, expands the schedule and adds K
+//          (sha.c:186-200 and the K of DO_ROUND, sha.c:57-69), writing W+K
+//          for 40 rounds at a time into an LDS slot, then the MD padding
+//          block(s) (sha.c:536-543);
+//   wave R runs the rounds from LDS and owns the state: 5 VALU per round
+//          (f, two rotations, add3, add) + 20 ds_read_b128 per block.
+// Two 10 KiB slots, one s_barrier per half block: S fills slot h while R
+// consumes slot h^1.  Same arithmetic as compress(); only the work split
+// differs.  Like k_sha1_fixed it takes an optional shorter tail chunk.
+template <int T>
+__device__ __forceinline__ constexpr uint32_t kconst() {
+  return T < 20 ? 0x5a827999u : T < 40 ? 0x6ed9eba1u : T < 60 ? 0x8f1bbcdcu : 0xca62c1d6u;  // sha.c:66-69
+}
+
+template <int T>
+__device__ __forceinline__ void round_wk(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
+                                         uint32_t wk) {
+  uint32_t f;
+  if constexpr (T < 20) f = f_ch(b, c, d);
+  else if constexpr (T < 40) f = f_par(b, c, d);
+  else if constexpr (T < 60) f = f_maj(b, c, d);
+  else f = f_par(b, c, d);
+  const uint32_t t = rotl(a, 5) + (f + e + wk);
+  e = d;
+  d = c;
+  c = rotl(b, 30);
+  b = a;
+  a = t;
+}
+
+// Rounds T..TEND-1 from slot (4 W+K words per 16-byte LDS entry, lane-major).
+template <int T, int TEND>
+__device__ __forceinline__ void consume_wk(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
+                                           const u32x4 *slot, uint32_t lane) {
+  if constexpr (T < TEND) {
+    const u32x4 q = slot[((T % 40) / 4) * 64 + lane];
+    round_wk<T>(a, b, c, d, e, q.x);
+    round_wk<T + 1>(a, b, c, d, e, q.y);
+    round_wk<T + 2>(a, b, c, d, e, q.z);
+    round_wk<T + 3>(a, b, c, d, e, q.w);
+    consume_wk<T + 4, TEND>(a, b, c, d, e, slot, lane);
+  }
+}
+
+template <int T, int TEND>
+__device__ __forceinline__ void produce_wk(uint32_t (&w)[16], u32x4 *slot, uint32_t lane) {
+  if constexpr (T < TEND) {
+    u32x4 q;
+    q.x = sched<T>(w) + kconst<T>();
+    q.y = sched<T + 1>(w) + kconst<T + 1>();
+    q.z = sched<T + 2>(w) + kconst<T + 2>();
+    q.w = sched<T + 3>(w) + kconst<T + 3>();
+    slot[((T % 40) / 4) * 64 + lane] = q;
+    produce_wk<T + 4, TEND>(w, slot, lane);
+  }
+}
+
+// One block through S: two half-block slots, one barrier each.
+__device__ __forceinline__ void produce_block(uint32_t (&w)[16], u32x4 (*lds)[10 * 64], uint32_t lane) {
+  produce_wk<0, 40>(w, lds[0], lane);
+  __syncthreads();
+  produce_wk<40, 80>(w, lds[1], lane);
+  __syncthreads();
+}
+
+template <bool VERIFY>
+__global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ base, uint64_t n_chunks, uint32_t pitch,
+                                                  uint32_t len, uint8_t *__restrict__ digests,
+                                                  const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok,
+                                                  uint32_t tail_len) {
+  __shared__ u32x4 lds[2][10 * 64];  // 2 slots x 40 words x 64 lanes = 20 KiB
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint64_t chunk0 = (uint64_t)blockIdx.x * 64u;  // workgroup-uniform: both waves agree
+  uint32_t nvalid;
+  if (chunk0 < n_chunks) {
+    const uint64_t left = n_chunks - chunk0;
+    nvalid = left < 64 ? (uint32_t)left : 64u;
+  } else {
+    if (tail_len == 0 || chunk0 != ((n_chunks + 63u) & ~(uint64_t)63u)) return;
+    chunk0 = n_chunks;
+    nvalid = 1;
+    len = tail_len;
+  }
+  const uint32_t nblocks = len >> 6, r = len & 63u;
+  const uint32_t nb_total = nblocks + (r >= 56u ? 2u : 1u);  // + MD padding block(s)
+  if (wave == 0) {
+    // ---- S: loads, schedule + K --------------------------------------------
+    const uint32_t mine = lane < nvalid ? lane : nvalid - 1u;
+    const uint32_t voff = mine * pitch;
+    const uint32_t nrec = (nvalid - 1u) * pitch + ((len + 3u) & ~3u);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(base + chunk0 * (uint64_t)pitch), (short)0, (int)nrec, 0x00020000);
+    // Four-block register ring, three blocks of prefetch (~2.5 us at R's
+    // pace): S must never stall on memory, or R waits at the barrier.  Loads
+    // past nrec are range-checked zeros, so they need no guard (and no branch
+    // that would make the compiler wait for them, see absorb_ring).
+    u32x4 ring[4][4];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ring[k][i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, k * 64u + 16u * i, 0);
+    for (uint32_t b = 0; b < nblocks; b += 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          ring[(k + 3) % 4][i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, (b + k + 3) * 64u + 16u * i, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (b + k < nblocks) {  // wave-uniform
+          uint32_t w[16];
+          block_from_le(w, ring[k][0], ring[k][1], ring[k][2], ring[k][3]);
+          produce_block(w, lds, lane);
+        }
+      }
+    }
+    // Tail bytes + MD padding (sha.c:536-543), as finish() lays them out.
+    uint32_t tail[16];
+    load_tail(tail, rsrc, voff, nblocks, r);
+    const uint32_t wi = r >> 2, mark = 0x80000000u >> ((r & 3) * 8);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) tail[j] |= (j == (int)wi) ? mark : 0u;
+    const uint64_t bits = (uint64_t)len * 8ull;
+    if (r >= 56u) {
+      produce_block(tail, lds, lane);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) tail[j] = 0u;
+    }
+    tail[14] = (uint32_t)(bits >> 32);
+    tail[15] = (uint32_t)bits;
+    produce_block(tail, lds, lane);
+    __syncthreads();  // pairs with R's last barrier
+  } else {
+    // ---- R: rounds -----------------------------------------------------------
+    State st;
+    st.init();
+    __syncthreads();  // slot 0 of block 0 is ready
+    for (uint32_t b = 0; b < nb_total; ++b) {
+      uint32_t a = st.h0, bb = st.h1, c = st.h2, d = st.h3, e = st.h4;
+      consume_wk<0, 40>(a, bb, c, d, e, lds[0], lane);
+      __syncthreads();
+      consume_wk<40, 80>(a, bb, c, d, e, lds[1], lane);
+      __syncthreads();
+      st.h0 += a;  // sha.c:446-450
+      st.h1 += bb;
+      st.h2 += c;
+      st.h3 += d;
+      st.h4 += e;
+    }
+    store_digest<VERIFY>(st, lane, nvalid, chunk0, digests, expected, ok);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -502,6 +677,23 @@ static hipError_t launch_lds(const void *d_in, uint64_t n, uint32_t pitch, uint3
                        len, d_dig, d_exp, d_ok);
   return hipGetLastError();
 }
+static hipError_t launch_lat(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
+                             const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, uint32_t tail_len) {
+  const uint64_t grid = (n + 63) / 64 + (tail_len ? 1 : 0);
+  if (d_ok)
+    hipLaunchKernelGGL((k_sha1_lat<true>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_in, n, pitch, len,
+                       d_dig, d_exp, d_ok, tail_len);
+  else
+    hipLaunchKernelGGL((k_sha1_lat<false>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_in, n, pitch, len,
+                       d_dig, d_exp, d_ok, tail_len);
+  return hipGetLastError();
+}
+
+// Batches of at most this many chunks take the latency kernel (0: never).
+static uint64_t g_lat_max = BT_SHA1_LATENCY_BATCH_DEFAULT;
+void btsha1_set_latency_batch(uint64_t max_chunks) { __atomic_store_n(&g_lat_max, max_chunks, __ATOMIC_RELAXED); }
+uint64_t btsha1_latency_batch() { return __atomic_load_n(&g_lat_max, __ATOMIC_RELAXED); }
+
 constexpr int kLdsVariant = 1010;  // bt_sha1_set_variant(10, 1, 0): LDS-staged k_sha1_lds
 constexpr int kLdsNtVariant = 1011;  // bt_sha1_set_variant(10, 1, 1): the same with nt DMA loads
 
@@ -521,6 +713,7 @@ hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uin
                                const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant, uint32_t tail_len) {
   if (tail_len && d_ok) return hipErrorInvalidValue;  // verify batches are whole chunks
   if (n == 0 && tail_len == 0) return hipSuccess;
+  if (n + (tail_len ? 1 : 0) <= btsha1_latency_batch()) return launch_lat(d_in, n, pitch, len, d_dig, d_exp, d_ok, s, tail_len);
   if (variant == kLdsVariant || variant == kLdsNtVariant) {
     if (n) {
       const hipError_t e = variant == kLdsVariant ? launch_lds<0>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s)

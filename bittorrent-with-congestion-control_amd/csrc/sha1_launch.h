@@ -12,6 +12,11 @@
 hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
                                const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant,
                                uint32_t tail_len = 0);
+// Batches of at most max_chunks chunks (tail included) take the latency kernel
+// k_sha1_lat instead of the selected variant; 0 disables it.
+#define BT_SHA1_LATENCY_BATCH_DEFAULT 16384
+void btsha1_set_latency_batch(uint64_t max_chunks);
+uint64_t btsha1_latency_batch();
 // Hot-kernel variant code = ring slots*100 + lines per slot*10 + nt flag.
 bool btsha1_fixed_variant_ok(int code);
 // n messages at d_base + d_off[i], d_len[i] bytes each; with d_off == NULL,

@@ -52,6 +52,11 @@ int bt_sha1_set_ring_depth(int nbuf);
 /* Hot-kernel variant: nbuf ring slots of `lines` 128-byte lines each, nt = 1
  * for non-temporal loads.  Returns -1 for a combination not compiled in. */
 int bt_sha1_set_variant(int nbuf, int lines, int nt);
+/* Batches of at most max_chunks chunks take the latency kernel (a loader /
+ * schedule wave and a round wave per 64 chunks, meeting in LDS), which
+ * shortens a lone chunk's serial chain; larger batches take the hot-kernel
+ * variant above.  0 disables it; default 16384.  Returns the previous value. */
+uint64_t bt_sha1_set_latency_batch(uint64_t max_chunks);
 
 /* ---- device-resident batches (the hot path) ---------------------------- */
 /* n chunks of chunk_len bytes, chunk i at d_in + i*pitch (pitch >= chunk_len).

@@ -1,5 +1,6 @@
 """GPU parity: the HIP path (through the C-ABI) against the oracle and the
 reference's golden vectors.  Bit-exact everywhere (integer/byte work)."""
+import contextlib
 import ctypes
 import hashlib
 import os
@@ -137,14 +138,30 @@ def synth4096(bt, torch, oracle):
 
 
 LDS = 10  # bt_sha1_set_ring_depth(10): the LDS-staged hot kernel (k_sha1_lds)
+LAT = "lat"  # bt_sha1_set_latency_batch: the two-wave latency kernel (k_sha1_lat)
 
 
-@pytest.mark.parametrize("variant", [(2, 1, 0), (3, 1, 0), (4, 1, 0), (2, 2, 0), (3, 1, 1), (LDS, 1, 0), (LDS, 1, 1)])
+@contextlib.contextmanager
+def kernel_mode(bt, mode):
+    """Pin the fixed-layout launches to one kernel: LAT, a ring depth or a
+    (nbuf, lines, nt) variant (latency kernel off).  Restores the defaults."""
+    prev = bt.set_latency_batch(1 << 62 if mode == LAT else 0)
+    if mode != LAT:
+        bt.set_variant(*(mode if isinstance(mode, tuple) else (mode, 1, 0)))
+    try:
+        yield
+    finally:
+        bt.set_variant(3, 1, 0)
+        bt.set_latency_batch(prev)
+
+
+@pytest.mark.parametrize("variant", [(2, 1, 0), (3, 1, 0), (4, 1, 0), (2, 2, 0), (3, 1, 1), (LDS, 1, 0), (LDS, 1, 1),
+                                     LAT])
 def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, variant):
     """BASELINE config 2: 4096 synthetic 512 KiB chunks, every digest == sha.c's,
-    for every compiled hot-kernel variant (ring depth, slot lines, nt, LDS-staged)."""
-    bt.set_variant(*variant)
-    try:
+    for every compiled hot-kernel variant (ring depth, slot lines, nt, LDS-staged)
+    and the latency kernel."""
+    with kernel_mode(bt, variant):
         n = 4096
         out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
         bt.chunks_dev(synth4096.data_ptr(), n, CHUNK, CHUNK, out.data_ptr())
@@ -152,17 +169,12 @@ def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, variant):
         raw = out.cpu().numpy().tobytes()
         got = [(str(i), raw[20 * i:20 * i + 20].hex()) for i in range(n)]
         assert got == read_pairs("synth4096.txt")
-    finally:
-        bt.set_ring_depth(3)
 
 
-@pytest.mark.parametrize("ring", [3, LDS])
+@pytest.mark.parametrize("ring", [3, LDS, LAT])
 def test_verify_dev_flags_mismatches(bt, torch, synth4096, ring):
-    bt.set_ring_depth(ring)
-    try:
+    with kernel_mode(bt, ring):
         _verify_dev_flags_mismatches(bt, torch, synth4096)
-    finally:
-        bt.set_ring_depth(3)
 
 
 def _verify_dev_flags_mismatches(bt, torch, synth4096):
@@ -190,39 +202,40 @@ def _verify_dev_flags_mismatches(bt, torch, synth4096):
     (1000, 1003, 67),            # odd pitch -> generic kernel
     (CHUNK, CHUNK + 256, 65),    # padded pitch, fast kernel
 ])
-@pytest.mark.parametrize("ring", [3, LDS])
+@pytest.mark.parametrize("ring", [3, LDS, LAT])
 def test_fixed_layouts_vs_oracle(bt, torch, oracle, chunk_len, pitch, n, ring):
     total = pitch * (n - 1) + chunk_len
     host = bytearray(oracle.fill_synthetic(total, 11, 0xC0FFEE))
     d = to_dev(torch, bytes(host))
     out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
-    bt.set_ring_depth(ring)
-    try:
+    with kernel_mode(bt, ring):
         bt.chunks_dev(d.data_ptr(), n, chunk_len, pitch, out.data_ptr())
         torch.cuda.synchronize()
-    finally:
-        bt.set_ring_depth(3)
     want = [oracle.sha1(bytes(host[i * pitch:i * pitch + chunk_len])) for i in range(n)]
     assert digests_of(torch, out, n) == want
 
 
+def _ragged_line_counts(bt, torch, oracle, ring):
+    deepest = 4 if ring in (LDS, LAT) else ring
+    for blocks in range(0, 2 * 2 * deepest + 3):
+        for r in (0, 5, 56):
+            L = 64 * blocks + r
+            n = 70
+            pitch = (L + 15) // 16 * 16 or 16
+            host = bytearray(oracle.fill_synthetic(pitch * n, blocks, deepest))
+            d = to_dev(torch, bytes(host))
+            out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+            bt.chunks_dev(d.data_ptr(), n, L, pitch, out.data_ptr())
+            torch.cuda.synchronize()
+            got = digests_of(torch, out, n)
+            for i in (0, 1, 63, 64, 69):
+                assert got[i] == oracle.sha1(bytes(host[i * pitch:i * pitch + L])), (ring, L, i)
+
+
 def test_every_ring_depth_on_ragged_line_counts(bt, torch, oracle):
-    for ring in (2, 3, 4, LDS):
-        bt.set_ring_depth(ring)
-        for blocks in range(0, 2 * 2 * min(ring, 4) + 3):
-            for r in (0, 5, 56):
-                L = 64 * blocks + r
-                n = 70
-                pitch = (L + 15) // 16 * 16 or 16
-                host = bytearray(oracle.fill_synthetic(pitch * n, blocks, ring))
-                d = to_dev(torch, bytes(host))
-                out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
-                bt.chunks_dev(d.data_ptr(), n, L, pitch, out.data_ptr())
-                torch.cuda.synchronize()
-                got = digests_of(torch, out, n)
-                for i in (0, 1, 63, 64, 69):
-                    assert got[i] == oracle.sha1(bytes(host[i * pitch:i * pitch + L])), (ring, L, i)
-    bt.set_ring_depth(3)
+    for ring in (2, 3, 4, LDS, LAT):
+        with kernel_mode(bt, ring):
+            _ragged_line_counts(bt, torch, oracle, ring)
 
 
 def test_host_pipeline_c_tar_and_tail(bt, oracle):
@@ -240,20 +253,18 @@ def test_host_pipeline_c_tar_and_tail(bt, oracle):
     assert bt.chunks_host(big, chunk_len=4096) == oracle.hash_chunks(big, 4096)
 
 
-@pytest.mark.parametrize("variant", [(3, 1, 0), (2, 2, 0), (LDS, 1, 0)])
+@pytest.mark.parametrize("variant", [(3, 1, 0), (2, 2, 0), (LDS, 1, 0), LAT])
 def test_image_tail_in_same_launch(bt, oracle, variant):
-    """launch_image: the short last chunk rides in the hot kernel's tail wave
-    (the LDS-staged variant hands it to the ragged kernel instead)."""
-    bt.set_variant(*variant)
-    try:
+    """launch_image: the short last chunk rides in the hot kernel's (or the
+    latency kernel's) tail wave; the LDS-staged variant hands it to the ragged
+    kernel instead."""
+    with kernel_mode(bt, variant):
         for chunk_len in (4096, 64 * 1024):
             for nfull in (0, 1, 63, 64, 65, 130):
                 for rem in (1, 3, 55, 56, 63, 64, 65, 1000, chunk_len - 1):
                     img = bytes(oracle.fill_synthetic(nfull * chunk_len + rem, nfull + rem, 0x7A11))
                     assert bt.chunks_host(img, chunk_len=chunk_len) == oracle.hash_chunks(img, chunk_len), \
                         (variant, chunk_len, nfull, rem)
-    finally:
-        bt.set_variant(3, 1, 0)
 
 
 def test_make_chunks_file_api(bt, oracle, tmp_path):

@@ -15,6 +15,8 @@ one JSON line per measurement (median of --reps):
   ragged_4096_u     the same lengths at arbitrary byte offsets
   update_1484       SHA1Update of one 512 KiB chunk fed as 1484-byte payloads
                     (save_data_packet's granule, util.c:275) + SHA1Final
+  batch_<n>_<mode>  n device-resident 512 KiB chunks through the hot kernel
+                    (fixed) or the two-wave latency kernel (lat), kernel time
   verifier_b1       bt_sha1_verifier with batch 1: submit -> verdict
 Digests are checked against the oracle (hashlib is not used).
 """
@@ -122,6 +124,37 @@ def main():
         ts.append(time.perf_counter() - t0)
     assert got == want
     emit("update_1484", ts)
+
+    # Device-resident batches of n 512 KiB chunks: the two-wave latency kernel
+    # (k_sha1_lat) against the hot kernel (k_sha1_fixed), kernel time only.
+    nmax = 65536
+    big = torch.empty(nmax * CHUNK, dtype=torch.uint8, device="cuda")
+    bt.fill_synthetic(big.data_ptr(), nmax * CHUNK, 0, orc.SEED_SYNTH, s.cuda_stream)
+    dig = torch.zeros(20 * nmax, dtype=torch.uint8, device="cuda")
+    golden = {}
+    gpath = os.path.join(REPO, "tests", "golden", "synth4096.txt")
+    for line in open(gpath):
+        if not line.startswith("#"):
+            i, h = line.split()
+            golden[int(i)] = h
+    prev = bt.set_latency_batch(0)
+    for n in (1, 64, 1024, 4096, 16384, 32768, 65536):
+        for mode, thr in (("fixed", 0), ("lat", 1 << 62)):
+            bt.set_latency_batch(thr)
+            res = []
+            for _ in range(max(3, args.reps // 2) + 1):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                bt.chunks_dev(big.data_ptr(), n, CHUNK, CHUNK, dig.data_ptr(), s.cuda_stream)
+                b.record(s)
+                torch.cuda.synchronize()
+                res.append(a.elapsed_time(b) * 1e-3)
+            raw = dig[:20 * min(n, 4096)].cpu().numpy().tobytes()
+            assert all(raw[20 * i:20 * i + 20].hex() == golden[i] for i in range(min(n, 4096))), (mode, n)
+            med = statistics.median(res[1:])
+            emit(f"batch_{n}_{mode}", res[1:], {"chunks": n, "GiB_per_s": round(n * CHUNK / med / 2**30, 2)})
+    bt.set_latency_batch(prev)
+    del big
 
     v = bt.Verifier(batch=1, nstreams=2)
     ts = []

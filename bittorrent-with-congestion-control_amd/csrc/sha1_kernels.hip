@@ -12,9 +12,14 @@
 //                   descriptor: per-lane 32-bit voffset = lane * pitch, the
 //                   line offset rides in the scalar soffset -> zero VALU
 //                   address arithmetic in the loop.
-//   k_sha1_ragged   arbitrary (offset, length) messages: shahash (chunk.c:33),
-//                   the short last chunk of make_chunks (chunk.c:20 when
-//                   fread returns < 512 KiB), ragged batches.
+//   k_sha1_lds      the hot path with coalesced LDS-DMA staging (a variant).
+//   k_sha1_lat      small fixed-layout batches (<= 16384 chunks: shahash,
+//                   small verify batches): a loader/schedule wave and a round
+//                   wave per 64 chunks meet in LDS, cutting a lone chain's
+//                   instruction count from 597 to ~426 per block.
+//   k_sha1_ragged   arbitrary (offset, length) messages and layouts the
+//                   fixed kernels do not take (pitch not a 16-byte multiple,
+//                   offsets past 4 GiB per wave).
 //   k_sha1_midstate chaining-state update over whole blocks: the GPU side of
 //                   the streaming SHA1Update/SHA1Final API (sha.c:453-558).
 //   k_fill_synthetic  frozen counter-based generator (bench/test data in HBM).

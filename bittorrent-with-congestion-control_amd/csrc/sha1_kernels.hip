@@ -297,9 +297,10 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
 //          block(s) (sha.c:536-543);
 //   wave R runs the rounds from LDS and owns the state: 5 VALU per round
 //          (f, two rotations, add3, add) + 20 ds_read_b128 per block.
-// Two 10 KiB slots, one s_barrier per half block: S fills slot h while R
-// consumes slot h^1.  Same arithmetic as compress(); only the work split
-// differs.  Like k_sha1_fixed it takes an optional shorter tail chunk.
+// Two 20 KiB slots of one block each, one s_barrier per block: S fills slot
+// b&1 while R consumes slot (b-1)&1.  Same arithmetic as compress(); only the
+// work split differs.  Like k_sha1_fixed it takes an optional shorter tail
+// chunk.
 template <int T>
 __device__ __forceinline__ constexpr uint32_t kconst() {
   return T < 20 ? 0x5a827999u : T < 40 ? 0x6ed9eba1u : T < 60 ? 0x8f1bbcdcu : 0xca62c1d6u;  // sha.c:66-69
@@ -321,12 +322,13 @@ __device__ __forceinline__ void round_wk(uint32_t &a, uint32_t &b, uint32_t &c, 
   a = t;
 }
 
-// Rounds T..TEND-1 from slot (4 W+K words per 16-byte LDS entry, lane-major).
+// Rounds T..TEND-1 from a block's slot (4 W+K words per 16-byte LDS entry,
+// lane-major).
 template <int T, int TEND>
 __device__ __forceinline__ void consume_wk(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
                                            const u32x4 *slot, uint32_t lane) {
   if constexpr (T < TEND) {
-    const u32x4 q = slot[((T % 40) / 4) * 64 + lane];
+    const u32x4 q = slot[(T / 4) * 64 + lane];
     round_wk<T>(a, b, c, d, e, q.x);
     round_wk<T + 1>(a, b, c, d, e, q.y);
     round_wk<T + 2>(a, b, c, d, e, q.z);
@@ -343,16 +345,15 @@ __device__ __forceinline__ void produce_wk(uint32_t (&w)[16], u32x4 *slot, uint3
     q.y = sched<T + 1>(w) + kconst<T + 1>();
     q.z = sched<T + 2>(w) + kconst<T + 2>();
     q.w = sched<T + 3>(w) + kconst<T + 3>();
-    slot[((T % 40) / 4) * 64 + lane] = q;
+    slot[(T / 4) * 64 + lane] = q;
     produce_wk<T + 4, TEND>(w, slot, lane);
   }
 }
 
-// One block through S: two half-block slots, one barrier each.
-__device__ __forceinline__ void produce_block(uint32_t (&w)[16], u32x4 (*lds)[10 * 64], uint32_t lane) {
-  produce_wk<0, 40>(w, lds[0], lane);
-  __syncthreads();
-  produce_wk<40, 80>(w, lds[1], lane);
+// One block through S into slot p, then the block's barrier.
+__device__ __forceinline__ void produce_block(uint32_t (&w)[16], u32x4 (*lds)[20 * 64], uint32_t &p, uint32_t lane) {
+  produce_wk<0, 80>(w, lds[p], lane);
+  p ^= 1u;
   __syncthreads();
 }
 
@@ -361,7 +362,7 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
                                                   uint32_t len, uint8_t *__restrict__ digests,
                                                   const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok,
                                                   uint32_t tail_len) {
-  __shared__ u32x4 lds[2][10 * 64];  // 2 slots x 40 words x 64 lanes = 20 KiB
+  __shared__ u32x4 lds[2][20 * 64];  // 2 slots x 80 words x 64 lanes = 40 KiB
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint64_t chunk0 = (uint64_t)blockIdx.x * 64u;  // workgroup-uniform: both waves agree
@@ -388,6 +389,7 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
     // pace): S must never stall on memory, or R waits at the barrier.  Loads
     // past nrec are range-checked zeros, so they need no guard (and no branch
     // that would make the compiler wait for them, see absorb_ring).
+    uint32_t slot = 0;
     u32x4 ring[4][4];
 #pragma unroll
     for (int k = 0; k < 3; ++k)
@@ -403,7 +405,7 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
         if (b + k < nblocks) {  // wave-uniform
           uint32_t w[16];
           block_from_le(w, ring[k][0], ring[k][1], ring[k][2], ring[k][3]);
-          produce_block(w, lds, lane);
+          produce_block(w, lds, slot, lane);
         }
       }
     }
@@ -415,24 +417,22 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
     for (int j = 0; j < 16; ++j) tail[j] |= (j == (int)wi) ? mark : 0u;
     const uint64_t bits = (uint64_t)len * 8ull;
     if (r >= 56u) {
-      produce_block(tail, lds, lane);
+      produce_block(tail, lds, slot, lane);
 #pragma unroll
       for (int j = 0; j < 16; ++j) tail[j] = 0u;
     }
     tail[14] = (uint32_t)(bits >> 32);
     tail[15] = (uint32_t)bits;
-    produce_block(tail, lds, lane);
+    produce_block(tail, lds, slot, lane);
     __syncthreads();  // pairs with R's last barrier
   } else {
     // ---- R: rounds -----------------------------------------------------------
     State st;
     st.init();
-    __syncthreads();  // slot 0 of block 0 is ready
+    __syncthreads();  // block 0 is in slot 0
     for (uint32_t b = 0; b < nb_total; ++b) {
       uint32_t a = st.h0, bb = st.h1, c = st.h2, d = st.h3, e = st.h4;
-      consume_wk<0, 40>(a, bb, c, d, e, lds[0], lane);
-      __syncthreads();
-      consume_wk<40, 80>(a, bb, c, d, e, lds[1], lane);
+      consume_wk<0, 80>(a, bb, c, d, e, lds[b & 1u], lane);
       __syncthreads();
       st.h0 += a;  // sha.c:446-450
       st.h1 += bb;

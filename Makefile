@@ -5,6 +5,9 @@ CSRC     := $(PKG)/csrc
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
+# Source id of the kernels (bt_sha1_source_id): profiles record it, bench.py
+# checks it before reusing PMC traffic measured on another build.
+SRC_ID   := $(shell cat $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h | sha256sum | cut -c1-16)
 LIB      := $(PKG)/libbtsha1.so
 BIN      := $(PKG)/bin
 
@@ -18,9 +21,10 @@ $(PKG)/build/sha1_kernels.o: $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h $(CS
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(PKG)/build/bt_sha1_api.o: $(CSRC)/bt_sha1_api.cpp $(CSRC)/sha1_launch.h include/bt_sha1.h include/sha.h include/chunk.h
+$(PKG)/build/bt_sha1_api.o: $(CSRC)/bt_sha1_api.cpp $(CSRC)/sha1_launch.h include/bt_sha1.h include/sha.h include/chunk.h \
+                           $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_SRC_ID='"$(SRC_ID)"' -c $< -o $@
 
 $(PKG)/build/bt_chunks.o: $(CSRC)/bt_chunks.cpp include/bt_sha1.h include/chunk.h
 	@mkdir -p $(dir $@)
@@ -46,11 +50,23 @@ oracle:
 # The reference's own make_chunks.c, unmodified, compiled against include/ and
 # linked to libbtsha1.so: the drop-in proof run by the gpu tests.  Built only
 # where the reference sources exist; the binary travels to the GPU box.
+# `-iquote include -I-` makes the reference's own `#include "chunk.h"` /
+# `"sha.h"` resolve to include/ (our drop-in headers) instead of the copies
+# next to the reference sources: the proof covers source compatibility too.
+DROPIN_INC := -iquote include -I- -I$(REF)
 ifneq ($(wildcard $(REF)/make_chunks.c),)
-dropin: oracle/_ref/make-chunks-dropin
+dropin: oracle/_ref/make-chunks-dropin oracle/_ref/save-chunk-dropin
 oracle/_ref/make-chunks-dropin: $(REF)/make_chunks.c $(LIB) include/chunk.h include/sha.h
 	@mkdir -p oracle/_ref
-	gcc -g -Wall -DDEBUG -DTESTING -Iinclude -o $@ $< -L$(PKG) -lbtsha1 -lm -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
+	gcc -g -Wall -DDEBUG -DTESTING $(DROPIN_INC) -o $@ $< -L$(PKG) -lbtsha1 -lm -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
+# Caller #2: the peer's receive/verify code (util.c:250-337) and file.c,
+# unmodified, with their reference flags (Makefile:2-5, plus -fcommon: the
+# reference headers define globals), linked to libbtsha1.so in place of
+# chunk.o + sha.o.  The harness plays peer.c's event loop for one GET.
+oracle/_ref/save-chunk-dropin: $(REF)/util.c $(REF)/file.c tests/native/save_chunk_harness.c $(LIB) include/chunk.h include/sha.h
+	@mkdir -p oracle/_ref
+	gcc -g -Wall -DDEBUG -DTESTING -fcommon $(DROPIN_INC) -o $@ $(REF)/util.c $(REF)/file.c tests/native/save_chunk_harness.c \
+	    -L$(PKG) -lbtsha1 -lm -Wl,--unresolved-symbols=ignore-in-object-files -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
 else
 dropin:
 	@echo "reference sources absent: using prebuilt oracle/_ref/make-chunks-dropin if present"

@@ -6,24 +6,35 @@ Workload (BASELINE config 3 per GPU, config 4 across GPUs): every rank holds
 HBM, generated in place by the frozen counter-based generator with GLOBAL
 chunk indices [rank*C, (rank+1)*C) (so N=8 is exactly config 4's 1 M chunks).
 One step = one launch of the hot kernel over all of the rank's chunks -> 20 B
-digests in HBM.  Weak scaling, no data-path collective: ranks only meet at the
-timing barriers, the max-over-ranks reduction, and a host-side (gloo) gather
-of digests after the timed region.
+digests in HBM.  Weak scaling, no data-path collective: ranks only meet on a
+CPU (gloo) group for the timing barriers, the max-over-ranks reduction and a
+host-side gather of digests after the timed region (shard.run_rank).
 
 Timed region: W untimed warmup steps, then barrier + synchronize, K steps,
 synchronize + barrier; value = all ranks' chunk bytes * K / max-over-ranks
 wall time, in GiB/s.  The hot kernel's own duration is also taken live with
-HIP events on the stream it is launched on (torch's current stream), for the
-roofline.  rank 0 at N=1 additionally times the reference sha.c
-(oracle/_ref/libref_sha1.so, compiled from the reference) on the host cores
-over a bounded sample of the same chunks, and cross-checks those digests.
+HIP events on the stream it is launched on, for the roofline.
+
+rank 0 at N=1 additionally reports, after the timed region:
+  * the in-kernel shader clock of the hot kernel (stamped diagnostic build,
+    bt_sha1_clock_probe), so the VALU roofline is priced at the clock the
+    chip actually held as well as at the nominal 2.4 GHz;
+  * cpu_baseline: the reference sha.c (oracle/_ref, compiled from the
+    reference) or our restatement (oracle/, "port") on the host cores, 4096
+    chunks of the same data at 1 thread and at every core this process may
+    use, at -O2 and at the reference Makefile's -O0 (SURVEY.md §8d);
+  * host_path: config 5, the PCIe-inclusive host->digest rates of the
+    pipelines that start in host memory (never `value`).
 """
 import argparse
 import ctypes
 import importlib.util
 import json
+import math
 import os
+import subprocess
 import sys
+import tempfile
 import threading
 import time
 
@@ -32,83 +43,112 @@ PKG = os.path.join(HERE, "bittorrent-with-congestion-control_amd")
 CHUNK = 512 * 1024
 SEED = 0x0B175EED
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
-VALU_OPS_PER_BLOCK = 597       # counted in the kernel's ISA
+VALU_OPS_PER_BLOCK = 597       # counted in the kernel's ISA (tests/test_isa.py)
 VALU_HALF_RATE_PER_BLOCK = 400  # v_alignbit / v_add3 / v_perm: 16 lanes/clk/SIMD (tools/ubench)
-VALU_FULL_RATE_PER_BLOCK = 197  # v_bitop3 / v_xor / v_add: 32 lanes/clk/SIMD with co-issue
+VALU_FULL_RATE_PER_BLOCK = 197  # v_bitop3 / v_xor / v_add: 32 lanes/clk/SIMD
 SIMDS, CLOCK_GHZ = 1024, 2.4
 # VALU ceiling for this exact instruction mix: a wave64 half-rate op holds the
 # SIMD 4 clocks, a full-rate op 2 -> 1994 clocks per 64-byte block per wave.
 _MIX_CLK = 4 * VALU_HALF_RATE_PER_BLOCK + 2 * VALU_FULL_RATE_PER_BLOCK
 VALU_MIX_PEAK_TOPS = VALU_OPS_PER_BLOCK * 64 * SIMDS * CLOCK_GHZ * 1e9 / _MIX_CLK / 1e12  # lane-ops/s, ~47.1
+METRIC = "GiB/s SHA-1 hashed (device-resident 512KiB chunks) at 1/2/4/8 MI355X"
 
 
-def load_btsha1():
-    if not os.path.exists(os.path.join(PKG, "libbtsha1.so")):  # clean checkout: build once
-        import fcntl
-        import subprocess
-        with open(os.path.join(HERE, ".build.lock"), "w") as lk:  # N ranks start together
-            fcntl.flock(lk, fcntl.LOCK_EX)
-            if not os.path.exists(os.path.join(PKG, "libbtsha1.so")):
-                subprocess.run(["make", "-C", HERE, "lib"], check=True)
-    spec = importlib.util.spec_from_file_location("btsha1", os.path.join(PKG, "btsha1.py"))
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
     mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
     spec.loader.exec_module(mod)
     return mod
 
 
-def cpu_baseline(host, n_chunks, gpu_digests, want_threads):
-    """Reference sha.c (or, if its prebuilt .so is absent, our port) on host cores."""
-    sys.path.insert(0, os.path.join(HERE, "oracle"))
-    import py_oracle
-    ref = py_oracle.load_reference("O2")
-    kind, flags = ("reference", "-O2 (reference chunk.c + sha.c)") if ref is not None else \
-        ("port", "-O2 (oracle/sha1_oracle.c)")
-    import numpy as np
-    base = host.ctypes.data
-    out = (ctypes.c_uint8 * (20 * n_chunks))()
-
-    def hash_range(lo, hi):
-        for i in range(lo, hi):
-            if ref is not None:
-                ref.shahash(ctypes.c_void_p(base + i * CHUNK), CHUNK, ctypes.byref(out, 20 * i))
-            else:
-                py_oracle._lib.or_shahash(ctypes.c_void_p(base + i * CHUNK), CHUNK, ctypes.byref(out, 20 * i))
-
-    def run(threads, n):
-        ts = [threading.Thread(target=hash_range, args=(n * t // threads, n * (t + 1) // threads))
-              for t in range(threads)]
-        t0 = time.perf_counter()
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-        return time.perf_counter() - t0
-
-    n1 = min(n_chunks, 2048)  # ~1.5 s on one core
-    t1 = run(1, n1)
-    tn = run(want_threads, n_chunks)
-    ok = bytes(out) == gpu_digests[:20 * n_chunks]
-    gib = n_chunks * CHUNK / 2**30
-    o0 = None  # the reference Makefile's own flags (-g, no -O): 1 thread, 256 chunks
-    ref0 = py_oracle.load_reference("O0")
-    if ref0 is not None:
-        n0 = min(n_chunks, 256)
-        o0_out = (ctypes.c_uint8 * 20)()
-        t0 = time.perf_counter()
-        for i in range(n0):
-            ref0.shahash(ctypes.c_void_p(base + i * CHUNK), CHUNK, o0_out)
-        o0 = round(n0 * CHUNK / 2**30 / (time.perf_counter() - t0), 4)
-    return {
-        "value": round(gib / tn, 4), "unit": "GiB/s", "cores": want_threads, "kind": kind,
-        "sample": f"{n_chunks} x 512 KiB chunks ({gib:.1f} GiB) of the same synthetic workload, "
-                  f"shahash per chunk, {want_threads} threads; 1 thread: "
-                  f"{round(n1 * CHUNK / 2**30 / t1, 4)} GiB/s",
-        "flags": flags, "digests_match_gpu": ok, "reference_O0_1thread_GiBs": o0,
-        "host_cpu": _cpu_model(),
-    }
+def ensure_built():
+    """A clean checkout has no built artefacts (git-ignored): build the library,
+    its host tools and the test-only oracle once (N ranks start together)."""
+    need = [os.path.join(PKG, "libbtsha1.so"), os.path.join(PKG, "bin", "verify-stream"),
+            os.path.join(HERE, "oracle", "liboracle_sha1.so"), os.path.join(HERE, "oracle", "liboracle_sha1_O0.so")]
+    if all(os.path.exists(p) for p in need):
+        return
+    import fcntl
+    with open(os.path.join(HERE, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not all(os.path.exists(p) for p in need):
+            subprocess.run(["make", "-C", HERE, "-j8", "lib", "tools", "oracle"], check=True)
 
 
-def _cpu_model():
+# ---------------------------------------------------------------------------
+# The HIP hasher one rank drives (shard.run_rank protocol).
+# ---------------------------------------------------------------------------
+class DeviceHasher:
+    def __init__(self, bt, torch, chunks, pitch, first_chunk):
+        self.bt, self.torch, self.C, self.pitch = bt, torch, chunks, pitch
+        self.buf = torch.empty(pitch * (chunks - 1) + CHUNK + 256, dtype=torch.uint8, device="cuda")
+        self.dig = torch.zeros(20 * chunks, dtype=torch.uint8, device="cuda")
+        # A dedicated stream: kernels and timing events share it.
+        self.stream = torch.cuda.Stream()
+        self.sp = self.stream.cuda_stream
+        if pitch == CHUNK:
+            bt.fill_synthetic(self.buf.data_ptr(), chunks * CHUNK, first_chunk * (CHUNK // 8), SEED, self.sp)
+        else:  # padded layout: fill chunk by chunk (same bytes per chunk)
+            for i in range(chunks):
+                bt.fill_synthetic(self.buf.data_ptr() + i * pitch, CHUNK, (first_chunk + i) * (CHUNK // 8), SEED, self.sp)
+        torch.cuda.synchronize()
+        self.ev = []
+
+    def step(self, i):
+        if i >= 0:
+            a, b = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
+            a.record(self.stream)
+            self.bt.chunks_dev(self.buf.data_ptr(), self.C, CHUNK, self.pitch, self.dig.data_ptr(), self.sp)
+            b.record(self.stream)
+            self.ev.append((a, b))
+        else:
+            self.bt.chunks_dev(self.buf.data_ptr(), self.C, CHUNK, self.pitch, self.dig.data_ptr(), self.sp)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def kernel_ms(self):
+        return sum(a.elapsed_time(b) for a, b in self.ev) / len(self.ev) if self.ev else None
+
+    def digests(self):
+        return self.dig.cpu().numpy().tobytes()
+
+    def clock_mhz(self, launches=3):
+        """Median in-kernel shader clock over the waves of the last of
+        `launches` back-to-back launches of the stamped build, right after the
+        timed region (MI355X_MICROARCH.md, DVFS item 6)."""
+        torch = self.torch
+        waves = (self.C + 63) // 64
+        st = torch.zeros(4 * waves, dtype=torch.int64, device="cuda")
+        scratch = torch.zeros(20 * self.C, dtype=torch.uint8, device="cuda")
+        for _ in range(launches):
+            self.bt.clock_probe(self.buf.data_ptr(), self.C, CHUNK, self.pitch, scratch.data_ptr(), st.data_ptr(), self.sp)
+        torch.cuda.synchronize()
+        s = st.view(-1, 4).cpu().double()
+        ratio = ((s[:, 2] - s[:, 0]) / (s[:, 3] - s[:, 1])).median().item()
+        same = bool(torch.equal(scratch, self.dig))
+        return ratio * self.bt.wallclock_khz() / 1000.0, same
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (SURVEY.md §8d)
+# ---------------------------------------------------------------------------
+def usable_cores():
+    """(threads this process may run on, machine CPUs, cgroup quota in CPUs or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, math.ceil(quota)))
+    return threads, os.cpu_count(), quota
+
+
+def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
@@ -118,6 +158,127 @@ def _cpu_model():
     return "unknown"
 
 
+def cpu_baseline(host_addr, n_chunks, gpu_digests):
+    """Reference sha.c (or our port when the reference objects are absent)
+    hashing n_chunks 512 KiB chunks at host_addr, shahash per chunk as
+    chunk.c:21 does, at 1 thread and at every usable core, -O2 and -O0."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import py_oracle  # test infrastructure: the checker / baseline, never the product
+    out = (ctypes.c_uint8 * (20 * n_chunks))()
+    threads, machine, quota = usable_cores()
+    gib = n_chunks * CHUNK / 2**30
+
+    def pick(opt):
+        ref = py_oracle.load_reference(opt)
+        if ref is not None:
+            return "reference", ref.shahash
+        port = py_oracle.load_port(opt)
+        return ("port", port.or_shahash) if port is not None else (None, None)
+
+    def run(fn, nthreads):
+        def hash_range(lo, hi):
+            for i in range(lo, hi):  # ctypes drops the GIL inside each call
+                fn(ctypes.c_void_p(host_addr + i * CHUNK), CHUNK, ctypes.byref(out, 20 * i))
+        ts = [threading.Thread(target=hash_range, args=(n_chunks * t // nthreads, n_chunks * (t + 1) // nthreads))
+              for t in range(nthreads)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        dt = time.perf_counter() - t0
+        return round(gib / dt, 4), bytes(out) == gpu_digests[:20 * n_chunks]
+
+    rows = {}
+    kind = None
+    for opt, flags in (("O2", "-O2"), ("O0", "-g -O0 (reference Makefile:3)")):
+        k, fn = pick(opt)
+        if fn is None:
+            continue
+        kind = kind or k
+        for nt in sorted({1, threads}):
+            rate, ok = run(fn, nt)
+            rows[f"{opt}_{nt}t"] = {"GiB_per_s": rate, "threads": nt, "flags": flags, "kind": k, "digests_match_gpu": ok}
+    best = rows.get(f"O2_{threads}t") or next(iter(rows.values()))
+    return {
+        "value": best["GiB_per_s"], "unit": "GiB/s", "cores": best["threads"], "kind": kind,
+        "sample": f"{n_chunks} x 512 KiB chunks ({gib:.1f} GiB) of the benchmark's own synthetic chunks, "
+                  f"shahash per chunk (chunk.c:21), static split over {threads} threads",
+        "flags": best["flags"], "digests_match_gpu": all(r["digests_match_gpu"] for r in rows.values()),
+        "runs": rows, "machine_cpus": machine, "affinity_cpus": len(os.sched_getaffinity(0)),
+        "cgroup_cpu_quota": quota, "host_cpu": cpu_model(),
+    }
+
+
+# ---------------------------------------------------------------------------
+# Host paths (config 5): PCIe-inclusive, starting in host memory
+# ---------------------------------------------------------------------------
+def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
+    """host: pageable numpy image of the first chunks of dev_buf; want: their
+    device-resident digests.  Each rate is the best of 2 runs (the first run
+    of a path also pays its one-time pinned staging allocation)."""
+    addr, nbytes = host.ctypes.data, host.nbytes
+    gib = nbytes / 2**30
+    out = {"image_GiB": round(gib, 3)}
+
+    def timed(fn, reps=2):
+        ts, ok = [], True
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            r = fn()
+            ts.append(time.perf_counter() - t0)
+            ok = ok and r == want
+        return round(gib / min(ts), 3), round(gib / ts[0], 3), ok
+
+    best, first, ok = timed(lambda: bt.chunks_host_addr(addr, nbytes))
+    out["pageable_chunks_host"] = {"GiB_per_s": best, "first_run_GiB_per_s": first, "digests_match": ok,
+                                   "path": "bt_sha1_chunks_host on pageable memory: threaded staging memcpy into "
+                                           "pinned lanes, 2-stream H2D, hot kernel, digests to pinned host"}
+    t0 = time.perf_counter()
+    bt.host_register(addr, nbytes)
+    reg_s = time.perf_counter() - t0
+    try:
+        best, first, ok = timed(lambda: bt.chunks_host_addr(addr, nbytes))
+        out["registered_direct_dma"] = {"GiB_per_s": best, "first_run_GiB_per_s": first, "digests_match": ok,
+                                        "register_s": round(reg_s, 3),
+                                        "path": "bt_sha1_host_register'ed image, H2D straight from it, 2 streams"}
+        pin = torch.from_numpy(host)
+        scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev_buf.device)
+        rates = []
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            scratch.copy_(pin, non_blocking=True)
+            torch.cuda.synchronize()
+            rates.append(gib / (time.perf_counter() - t0))
+        out["raw_h2d_ceiling"] = {"GiB_per_s": round(max(rates), 3), "path": "one hipMemcpy of the registered image"}
+    finally:
+        bt.host_unregister(addr)
+    # Zero-copy batched verifier (util.c:304-337 replacement): the product's C
+    # host tool, batch 1024 x 2 streams, over a 1 GiB image in a tmpfs file.
+    vs = os.path.join(PKG, "bin", "verify-stream")
+    n = min(int(verify_gib * 2**30) // CHUNK, nbytes // CHUNK)
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+    with tempfile.TemporaryDirectory(dir=shm) as d:
+        img, lst = os.path.join(d, "img"), os.path.join(d, "img.chunks")
+        host[:n * CHUNK].tofile(img)
+        with open(lst, "w") as f:
+            for i in range(n):
+                f.write(f"{i} {want[20 * i:20 * i + 20].hex()}\n")
+        rounds = 9
+        r = subprocess.run([vs, "-z", "-b", "1024", "-s", "2", "-r", str(rounds), img, lst],
+                           capture_output=True, text=True, timeout=300)
+        res = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {}
+        out["zero_copy_verifier"] = {
+            "GiB_per_s": res.get("GiB_per_s"), "digests_match": r.returncode == 0 and res.get("failed") == 0
+            and res.get("ok") == res.get("chunks"), "chunks_verified": res.get("chunks"),
+            "path": f"bin/verify-stream -z -b 1024 -s 2: {n} received chunks in pinned verifier slots, "
+                    f"{rounds - 1} steady-state rounds timed (H2D + hash + fused memcmp + verdicts)",
+            **({} if r.returncode == 0 else {"error": r.stderr[-300:]})}
+    return out
+
+
+# ---------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,12 +289,15 @@ def main():
     ap.add_argument("--lines", type=int, default=1, help="128-byte lines per ring slot (with --ring)")
     ap.add_argument("--nt", type=int, default=0, help="non-temporal loads (with --ring)")
     ap.add_argument("--pitch", type=int, default=CHUNK, help="bytes between chunk starts in HBM")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-chunks", type=int, default=32768,
-                    help="CPU-baseline sample: 16 GiB, ~25 core-seconds of reference sha.c")
+    ap.add_argument("--cpu-chunks", type=int, default=4096, help="CPU-baseline sample (SURVEY.md §8d: 4096 chunks)")
+    ap.add_argument("--host-gib", type=float, default=8.0, help="host-path image size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo for rehearsals)")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r01.json"))
+    ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--no-clock", action="store_true")
+    ap.add_argument("--backend", default="gloo",
+                    help="process group for the control plane (barriers, timings, digest gather); "
+                         "the hash path has no collective")
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r02.json"))
     args = ap.parse_args()
 
     import torch
@@ -144,162 +308,152 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = local % max(1, torch.cuda.device_count())  # == local on a full node
     torch.cuda.set_device(dev)
+    group = None
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-            cpu_group = dist.new_group(backend="gloo")
+            group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group(args.backend)
-            cpu_group = None
-    bt = load_btsha1()
+    if rank == 0:
+        ensure_built()
+    shard.barrier(world, group)
+    bt = _load("btsha1", os.path.join(PKG, "btsha1.py"))
     if args.ring:
         bt.set_variant(args.ring, args.lines, args.nt)
 
-    C = args.chunks
-    pitch = args.pitch
-    buf = torch.empty(pitch * (C - 1) + CHUNK + 256, dtype=torch.uint8, device="cuda")
-    dig = torch.zeros(20 * C, dtype=torch.uint8, device="cuda")
-    # A dedicated stream (torch's default stream has handle 0, which the C-ABI
-    # reads as "library stream"): kernels and timing events share it.
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
-    sp = stream.cuda_stream
-    assert sp != 0
-    first_chunk = rank * C
-    if pitch == CHUNK:
-        bt.fill_synthetic(buf.data_ptr(), C * CHUNK, first_chunk * (CHUNK // 8), SEED, sp)
-    else:  # padded layout: fill chunk by chunk (same bytes per chunk)
-        for i in range(C):
-            bt.fill_synthetic(buf.data_ptr() + i * pitch, CHUNK, (first_chunk + i) * (CHUNK // 8), SEED, sp)
-    torch.cuda.synchronize()
+    C, pitch = args.chunks, args.pitch
+    first_chunk, _ = shard.weak_range(rank, C)
+    hasher = DeviceHasher(bt, torch, C, pitch, first_chunk)
+    res = shard.run_rank(hasher, args.steps, args.warmup, world, rank, group)
 
-    def step():
-        bt.chunks_dev(buf.data_ptr(), C, CHUNK, pitch, dig.data_ptr(), sp)
+    line = None
+    if rank == 0:
+        all_dig = res["digests"]
+        wall_max, kern_max = res["wall_max"], res["kernel_ms_max"]
+        total_bytes = world * C * CHUNK * args.steps
+        value = total_bytes / wall_max / 2**30
+        bytes_per_launch = C * CHUNK
+        achieved = bytes_per_launch / (kern_max * 1e-3) / 1e9
+        valu_tops = C * (CHUNK // 64 + 1) * VALU_OPS_PER_BLOCK / (kern_max * 1e-3) / 1e12
+        kernel = bt.kernel_name(C)
 
-    for _ in range(args.warmup):
-        step()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(stream)
-        step()
-        b.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+        # Parity spot check of the timed output: global chunks 0..4095 are the
+        # committed golden vectors (tests/golden/synth4096.txt, from sha.c).
+        parity = None
+        golden = os.path.join(HERE, "tests", "golden", "synth4096.txt")
+        if os.path.exists(golden) and world * C >= 4096:
+            rows = [l.split() for l in open(golden) if not l.startswith("#")]
+            parity = all(all_dig[20 * int(i):20 * int(i) + 20].hex() == h for i, h in rows)
 
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
-    per_rank = [t.clone() for _ in range(world)]
-    if world > 1:
-        dist.all_gather(per_rank, t)  # config 4 wants per-GPU rates beside the aggregate
-    per_rank = [(float(x[0]), float(x[1])) for x in per_rank]
-    wall_max = max(w for w, _ in per_rank)
-    kern_max = max(k for _, k in per_rank)
+        clock = None
+        if world == 1 and not args.no_clock and kernel == "k_sha1_fixed":
+            mhz, same = hasher.clock_mhz()
+            clock = {"in_kernel_mhz": round(mhz, 1), "probe_digests_identical": same,
+                     "method": "stamped build of the hot kernel (bt_sha1_clock_probe): median over waves of "
+                               "delta s_memtime / delta s_memrealtime x wall-clock rate, 3 launches after the "
+                               "timed region"}
 
-    # Host-side gather of digests (after timing): rank order == global chunk order.
-    host_dig = dig.cpu()
-    if world > 1:
-        parts = [torch.empty_like(host_dig) for _ in range(world)] if rank == 0 else None
-        dist.gather(host_dig, parts, dst=0, group=cpu_group)
-        all_dig = torch.cat(parts).numpy().tobytes() if rank == 0 else None
-    else:
-        all_dig = host_dig.numpy().tobytes()
-
-    if rank != 0:
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
-
-    total_bytes = world * C * CHUNK * args.steps
-    value = total_bytes / wall_max / 2**30
-    bytes_per_launch = C * CHUNK
-    achieved = bytes_per_launch / (kern_max * 1e-3) / 1e9
-    # one lane-op per instruction per chunk-lane
-    valu_tops = C * (CHUNK // 64 + 1) * VALU_OPS_PER_BLOCK / (kern_max * 1e-3) / 1e12
-
-    # Parity spot check of the timed output: global chunks 0..4095 are the
-    # committed golden vectors (tests/golden/synth4096.txt, from sha.c).
-    parity = None
-    golden = os.path.join(HERE, "tests", "golden", "synth4096.txt")
-    if os.path.exists(golden) and C >= 4096:
-        rows = [l.split() for l in open(golden) if not l.startswith("#")]
-        parity = all(all_dig[20 * int(i):20 * int(i) + 20].hex() == h for i, h in rows)
-
-    traffic = None
-    traffic_src = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("chunks") == C and tj.get("pitch", CHUNK) == pitch:
-                traffic = tj.get("hbm_bytes_per_launch")
-                traffic_src = os.path.relpath(args.traffic_json, HERE)
-        except (OSError, ValueError):
-            pass
-
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        n = min(args.cpu_chunks, C)
-        import numpy as np
-        host = np.empty(n * CHUNK, dtype=np.uint8)
-        if pitch == CHUNK:
-            step = 2048 * CHUNK  # 1 GiB slices: no second full-size host copy
-            for o in range(0, n * CHUNK, step):
-                host[o:o + step] = buf[o:min(o + step, n * CHUNK)].cpu().numpy()
+        # PMC traffic, only when measured on this very build and layout.
+        traffic, traffic_note = None, None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                want = {"chunks": C, "pitch": pitch, "source_id": bt.source_id(), "kernel": kernel,
+                        "variant": bt.build_info().split("ring=")[1].split()[0]}
+                diff = {k: (tj.get(k), v) for k, v in want.items() if tj.get(k) != v}
+                if diff:
+                    traffic_note = f"{os.path.relpath(args.traffic_json, HERE)} was measured on another build/layout: {diff}"
+                else:
+                    traffic = tj.get("hbm_bytes_per_launch")
+                    traffic_note = f"{os.path.relpath(args.traffic_json, HERE)} (rocprofv3 --pmc, same source id)"
+            except (OSError, ValueError) as e:
+                traffic_note = f"unreadable: {e}"
         else:
-            for i in range(n):
-                host[i * CHUNK:(i + 1) * CHUNK] = buf[i * pitch:i * pitch + CHUNK].cpu().numpy()
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        cpu = cpu_baseline(host, n, all_dig, threads)
+            traffic_note = "no PMC traffic file for this build"
 
-    line = {
-        "metric": "GiB/s SHA-1 hashed (device-resident 512KiB chunks) at 1/2/4/8 MI355X",
-        "value": round(value, 3),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(wall_max * 1e3 / args.steps, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u32",
-        "data": "synthetic: device-generated splitmix64 stream (seed 0x0B175EED, global chunk index)",
-        "config": {
-            "workload": f"{C} x 512 KiB chunks per GPU, device-resident ({C * CHUNK / 2**30:.0f} GiB/GPU), "
-                        "one hot-kernel launch per step -> 20 B digests",
-            "chunks_per_gpu": C, "chunk_bytes": CHUNK, "pitch_bytes": pitch,
-            "global_chunks": world * C,
-            "parallelism": f"dp{world} (contiguous chunk-range split, no data-path collective)",
-            "kernel_variant": bt.build_info().split("hip")[-1].split(" ", 1)[-1],
-        },
-        "roofline": {
-            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "k_sha1_fixed", "kernel_ms": round(kern_max, 4),
-            "algorithmic_bytes_per_launch": bytes_per_launch, "traffic_source": traffic_src,
-        },
-        "valu_roofline": {"bound": "valu", "achieved": round(valu_tops, 2), "peak": round(VALU_MIX_PEAK_TOPS, 2),
-                          "unit": "T int32 lane-ops/s", "frac": round(valu_tops / VALU_MIX_PEAK_TOPS, 4),
-                          "ops_per_block": VALU_OPS_PER_BLOCK,
-                          "peak_basis": f"{VALU_OPS_PER_BLOCK}-instruction mix ({VALU_HALF_RATE_PER_BLOCK} half-rate, "
-                                        f"{VALU_FULL_RATE_PER_BLOCK} full-rate) at 2.4 GHz on 1024 SIMDs"},
-        "per_gpu": [{"rank": r, "GiB_per_s": round(C * CHUNK * args.steps / w / 2**30, 3),
-                     "kernel_ms": round(k, 4)} for r, (w, k) in enumerate(per_rank)],
-        "parity_first_4096_vs_golden": parity,
-        "cpu_baseline": cpu,
-    }
-    print(json.dumps(line), flush=True)
+        extras_host = None
+        if world == 1 and (not args.no_cpu_baseline or not args.no_host_path):
+            import numpy as np
+            n_host = min(C, max(args.cpu_chunks if not args.no_cpu_baseline else 0,
+                                0 if args.no_host_path else int(args.host_gib * 2**30) // CHUNK))
+            extras_host = np.empty(n_host * CHUNK, dtype=np.uint8)
+            view = torch.from_numpy(extras_host)
+            for i in range(0, n_host, 2048):  # 1 GiB slices
+                k = min(2048, n_host - i)
+                if pitch == CHUNK:
+                    view[i * CHUNK:(i + k) * CHUNK].copy_(hasher.buf[i * CHUNK:(i + k) * CHUNK])
+                else:
+                    for j in range(i, i + k):
+                        view[j * CHUNK:(j + 1) * CHUNK].copy_(hasher.buf[j * pitch:j * pitch + CHUNK])
+
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(extras_host.ctypes.data, min(args.cpu_chunks, C), all_dig)
+            except Exception as e:  # the checker must never cost the bench line
+                cpu = {"error": f"{type(e).__name__}: {e}"}
+
+        host = None
+        if world == 1 and not args.no_host_path and pitch == CHUNK:
+            try:
+                n_img = min(C, int(args.host_gib * 2**30) // CHUNK)
+                host = host_paths(bt, torch, hasher.buf, extras_host[:n_img * CHUNK], all_dig[:20 * n_img])
+            except Exception as e:
+                host = {"error": f"{type(e).__name__}: {e}"}
+
+        peak_at_clock = VALU_MIX_PEAK_TOPS * (clock["in_kernel_mhz"] / 1000.0 / CLOCK_GHZ) if clock else None
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: device-generated splitmix64 stream (seed 0x0B175EED, global chunk index)",
+            "config": {
+                "workload": f"{C} x 512 KiB chunks per GPU, device-resident ({C * CHUNK / 2**30:.0f} GiB/GPU), "
+                            "one hot-kernel launch per step -> 20 B digests",
+                "chunks_per_gpu": C, "chunk_bytes": CHUNK, "pitch_bytes": pitch,
+                "global_chunks": world * C,
+                "parallelism": f"dp{world} (contiguous chunk-range split, no data-path collective)",
+                "build": bt.build_info(),
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": kernel, "kernel_ms": round(kern_max, 4),
+                "algorithmic_bytes_per_launch": bytes_per_launch, "traffic_source": traffic_note,
+            },
+            "valu_roofline": {
+                "bound": "valu", "achieved": round(valu_tops, 2), "unit": "T int32 lane-ops/s",
+                "peak": round(VALU_MIX_PEAK_TOPS, 2), "frac": round(valu_tops / VALU_MIX_PEAK_TOPS, 4),
+                "peak_at_measured_clock": round(peak_at_clock, 2) if peak_at_clock else None,
+                "frac_at_measured_clock": round(valu_tops / peak_at_clock, 4) if peak_at_clock else None,
+                "ops_per_block": VALU_OPS_PER_BLOCK,
+                "peak_basis": f"{VALU_OPS_PER_BLOCK}-instruction mix ({VALU_HALF_RATE_PER_BLOCK} half-rate, "
+                              f"{VALU_FULL_RATE_PER_BLOCK} full-rate) on 1024 SIMDs at 2.4 GHz (peak) and at the "
+                              "in-kernel clock (peak_at_measured_clock)"},
+            "clock": clock,
+            "per_gpu": [{"rank": r, "GiB_per_s": round(C * CHUNK * args.steps / w / 2**30, 3),
+                         "kernel_ms": round(k, 4)} for r, (w, k) in enumerate(res["per_rank"])],
+            "parity_first_4096_vs_golden": parity,
+            "cpu_baseline": cpu,
+            "host_path": host,
+        }
+        print(json.dumps(line), flush=True)
     if world > 1:
-        dist.barrier()
+        shard.barrier(world, group)
         dist.destroy_process_group()
+    return line
 
+
+shard = _load("shard", os.path.join(PKG, "shard.py"))
 
 if __name__ == "__main__":
     main()

@@ -62,6 +62,11 @@ _sig("bt_sha1_chunks_host", _i64, _vp, _u64, _u64, _vp)
 _sig("bt_sha1_host_register", ctypes.c_int, _vp, _u64)
 _sig("bt_sha1_host_unregister", ctypes.c_int, _vp)
 _sig("bt_sha1_chunks_host_multi", _i64, _vp, _u64, _u64, _vp, ctypes.c_int)
+_sig("bt_sha1_chunks_host_devices", _i64, _vp, _u64, _u64, _vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int)
+_sig("bt_sha1_source_id", ctypes.c_char_p)
+_sig("bt_sha1_kernel_name", ctypes.c_char_p, _u64)
+_sig("bt_sha1_clock_probe", ctypes.c_int, _vp, _u64, _u64, _u64, _vp, _vp, _vp)
+_sig("bt_sha1_wallclock_khz", _i64)
 _sig("bt_sha1_chunks_file", _i64, _vp, _u64, _vp, _u64)
 _sig("bt_sha1_verifier_create", _vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32)
 _sig("bt_sha1_verifier_destroy", None, _vp)
@@ -124,6 +129,28 @@ def set_latency_batch(max_chunks):
 
 def build_info():
     return lib.bt_sha1_build_info().decode()
+
+
+def source_id():
+    """Id of the kernel sources compiled into the library (profiles record it)."""
+    return lib.bt_sha1_source_id().decode()
+
+
+def kernel_name(n_chunks):
+    """Kernel a fixed-layout batch of n_chunks runs on the current device."""
+    r = lib.bt_sha1_kernel_name(n_chunks)
+    if r is None:
+        raise BtSha1Error(f"bt_sha1_kernel_name: {last_error()}")
+    return r.decode()
+
+
+def clock_probe(d_in, n, chunk_len, pitch, d_digests, d_stamps, stream=None):
+    """Stamped diagnostic build of the hot kernel (4 uint64 per wave into d_stamps)."""
+    _check(lib.bt_sha1_clock_probe(d_in, n, chunk_len, pitch, d_digests, d_stamps, stream), "bt_sha1_clock_probe")
+
+
+def wallclock_khz():
+    return _check(lib.bt_sha1_wallclock_khz(), "bt_sha1_wallclock_khz")
 
 
 # ---- device-resident (addresses are ints) ------------------------------------
@@ -210,15 +237,24 @@ def _host_buf(data):
     return arr, mv.nbytes
 
 
-def chunks_host(data, chunk_len=CHUNK, ndev=None):
-    """Digests of data cut into chunk_len pieces (short last piece): list of 20-byte values."""
+def _host_split(addr, nbytes, chunk_len, out, ndev, devs):
+    if devs is not None:
+        arr = (ctypes.c_int * max(len(devs), 1))(*devs)
+        return _check(lib.bt_sha1_chunks_host_devices(addr, nbytes, chunk_len, out, arr, len(devs)),
+                      "bt_sha1_chunks_host_devices")
+    if ndev is not None:
+        return _check(lib.bt_sha1_chunks_host_multi(addr, nbytes, chunk_len, out, ndev), "bt_sha1_chunks_host_multi")
+    return _check(lib.bt_sha1_chunks_host(addr, nbytes, chunk_len, out), "bt_sha1_chunks_host")
+
+
+def chunks_host(data, chunk_len=CHUNK, ndev=None, devs=None):
+    """Digests of data cut into chunk_len pieces (short last piece): list of 20-byte values.
+    ndev: split over the first ndev GPUs; devs: split over this list of device
+    ids (repeats allowed: one worker per entry)."""
     buf, n = _host_buf(data)
     nch = (n + chunk_len - 1) // chunk_len
     out = (ctypes.c_uint8 * max(20 * nch, 1))()
-    if ndev is None:
-        got = _check(lib.bt_sha1_chunks_host(buf, n, chunk_len, out), "bt_sha1_chunks_host")
-    else:
-        got = _check(lib.bt_sha1_chunks_host_multi(buf, n, chunk_len, out, ndev), "bt_sha1_chunks_host_multi")
+    got = _host_split(buf, n, chunk_len, out, ndev, devs)
     raw = bytes(out)
     return [raw[20 * i:20 * i + 20] for i in range(got)]
 
@@ -232,14 +268,11 @@ def host_unregister(addr):
     _check(lib.bt_sha1_host_unregister(addr), "bt_sha1_host_unregister")
 
 
-def chunks_host_addr(addr, nbytes, chunk_len=CHUNK, ndev=None):
+def chunks_host_addr(addr, nbytes, chunk_len=CHUNK, ndev=None, devs=None):
     """bt_sha1_chunks_host over raw host memory at `addr` (no copy on the Python side)."""
     nch = (nbytes + chunk_len - 1) // chunk_len
     out = (ctypes.c_uint8 * max(20 * nch, 1))()
-    if ndev is None:
-        got = _check(lib.bt_sha1_chunks_host(addr, nbytes, chunk_len, out), "bt_sha1_chunks_host")
-    else:
-        got = _check(lib.bt_sha1_chunks_host_multi(addr, nbytes, chunk_len, out, ndev), "bt_sha1_chunks_host_multi")
+    got = _host_split(addr, nbytes, chunk_len, out, ndev, devs)
     return bytes(out)[:20 * got]
 
 

@@ -136,6 +136,9 @@ struct DevCtx {
 
 std::mutex g_ctx_mu;
 std::vector<std::unique_ptr<DevCtx>> g_ctx;
+// Extra worker contexts (own streams and staging) for a device listed more
+// than once in bt_sha1_chunks_host_devices; index k-1 = its k-th repeat.
+std::vector<std::vector<std::unique_ptr<DevCtx>>> g_extra;
 
 int device_count() {
   int n = 0;
@@ -168,6 +171,22 @@ DevCtx *ctx_for(int dev) {
   return g_ctx[dev].get();
 }
 
+// Context for the k-th use of `dev` inside one multi-device call (k = 0 is the
+// device's own context, shared with every other entry point).
+DevCtx *worker_ctx(int dev, int k) {
+  DevCtx *base = ctx_for(dev);
+  if (!base || k == 0) return base;
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  if ((int)g_extra.size() <= dev) g_extra.resize(dev + 1);
+  auto &v = g_extra[dev];
+  while ((int)v.size() < k) {
+    auto c = std::make_unique<DevCtx>();
+    c->dev = dev;
+    v.push_back(std::move(c));
+  }
+  return v[k - 1].get();
+}
+
 // Streams are created on first use and kept few: HIP multiplexes streams onto
 // GPU_MAX_HW_QUEUES (4) hardware queues, and two streams that share a queue
 // serialise -- which silently kills the H2D/hash overlap of the pipelines.
@@ -182,11 +201,12 @@ int ensure_streams(DevCtx *c) {
   return 0;
 }
 
-hipStream_t pick_stream(void *stream, DevCtx *c) {
-  if (stream) return (hipStream_t)stream;
-  if (ensure_streams(c)) return nullptr;
-  return c->s;
-}
+// Caller streams of the device-resident entry points.  NULL is the device's
+// null (default) stream, exactly as for a hipLaunchKernelGGL(..., 0, ...) of the
+// caller's own: ordered after the caller's earlier default-stream work (e.g.
+// torch's default stream, whose handle is 0) and before its later work.  The
+// library's own non-blocking streams serve only its host pipelines.
+hipStream_t pick_stream(void *stream) { return (hipStream_t)stream; }
 
 bool fast_layout(const void *d_in, uint64_t chunk_len, uint64_t pitch, const void *d_dig) {
   return ((uintptr_t)d_in & 15) == 0 && (pitch & 15) == 0 && ((uintptr_t)d_dig & 3) == 0 &&
@@ -444,9 +464,10 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   return (int64_t)next;
 }
 
-int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t chunk_len, uint8_t *h_dig) {
+int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t chunk_len, uint8_t *h_dig,
+                       int worker = 0) {
   KeepDevice keep_dev;
-  DevCtx *c = ctx_for(dev);
+  DevCtx *c = worker_ctx(dev, worker);
   if (!c) return -1;
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(dev) != hipSuccess) {
@@ -591,19 +612,65 @@ int bt_sha1_set_device(int device) {
 
 const char *bt_sha1_last_error(void) { return t_err.c_str(); }
 
+#ifndef BT_SHA1_SRC_ID
+#define BT_SHA1_SRC_ID "unknown"
+#endif
+
 const char *bt_sha1_build_info(void) {
-  static char info[128];
-  snprintf(info, sizeof info, "libbtsha1 gfx950 hip%d.%d ring=%d latency_batch=%llu", HIP_VERSION_MAJOR,
-           HIP_VERSION_MINOR, g_variant.load(), (unsigned long long)btsha1_latency_batch());
+  static thread_local char info[192];
+  const uint64_t lat = btsha1_latency_batch_setting();
+  char latbuf[48];
+  if (lat == BT_SHA1_LATENCY_AUTO)
+    snprintf(latbuf, sizeof latbuf, "auto");
+  else
+    snprintf(latbuf, sizeof latbuf, "%llu", (unsigned long long)lat);
+  snprintf(info, sizeof info, "libbtsha1 gfx950 hip%d.%d ring=%d latency_batch=%s src=%s", HIP_VERSION_MAJOR,
+           HIP_VERSION_MINOR, g_variant.load(), latbuf, BT_SHA1_SRC_ID);
   return info;
 }
+
+const char *bt_sha1_source_id(void) { return BT_SHA1_SRC_ID; }
 
 int bt_sha1_set_ring_depth(int nbuf) { return bt_sha1_set_variant(nbuf, 1, 0); }
 
 uint64_t bt_sha1_set_latency_batch(uint64_t max_chunks) {
-  const uint64_t prev = btsha1_latency_batch();
+  const uint64_t prev = btsha1_latency_batch_setting();
   btsha1_set_latency_batch(max_chunks);
   return prev;
+}
+
+const char *bt_sha1_kernel_name(uint64_t n_chunks) {
+  if (device_count() <= 0) {
+    set_err("no HIP device visible");
+    return nullptr;
+  }
+  return btsha1_fixed_kernel_name(n_chunks, g_variant.load());
+}
+
+int bt_sha1_clock_probe(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_t pitch, uint8_t *d_digests,
+                        uint64_t *d_stamps, void *stream) {
+  if (n == 0) return 0;
+  if (!d_in || !d_digests || !d_stamps) {
+    set_err("null pointer");
+    return -1;
+  }
+  if (!fast_layout(d_in, chunk_len, pitch, d_digests)) {
+    set_err("clock probe needs the hot kernel's layout");
+    return -1;
+  }
+  int dev = 0;
+  BT_CK(hipGetDevice(&dev));
+  if (!ctx_for(dev)) return -1;
+  BT_CK(btsha1_launch_fixed_stamped(d_in, n, (uint32_t)pitch, (uint32_t)chunk_len, d_digests, d_stamps,
+                                    pick_stream(stream), g_variant.load()));
+  return 0;
+}
+
+int64_t bt_sha1_wallclock_khz(void) {
+  int dev = 0, khz = 0;
+  BT_CK(hipGetDevice(&dev));
+  BT_CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  return khz;
 }
 
 int bt_sha1_set_variant(int nbuf, int lines, int nt) {
@@ -631,8 +698,7 @@ int bt_sha1_chunks_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_
   BT_CK(hipGetDevice(&dev));
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
-  hipStream_t st = pick_stream(stream, c);
-  if (!st) return -1;
+  hipStream_t st = pick_stream(stream);
   return launch_chunks(d_in, n, chunk_len, pitch, d_digests, st);
 }
 
@@ -651,8 +717,7 @@ int bt_sha1_verify_dev(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_
   BT_CK(hipGetDevice(&dev));
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
-  hipStream_t st = pick_stream(stream, c);
-  if (!st) return -1;
+  hipStream_t st = pick_stream(stream);
   BT_CK(btsha1_launch_fixed(d_in, n, (uint32_t)pitch, (uint32_t)chunk_len, d_digests, d_expected, d_ok, st,
                             g_variant.load()));
   return 0;
@@ -669,8 +734,7 @@ int bt_sha1_ragged_dev(const void *d_base, const uint64_t *d_offsets, const uint
   BT_CK(hipGetDevice(&dev));
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
-  hipStream_t st = pick_stream(stream, c);
-  if (!st) return -1;
+  hipStream_t st = pick_stream(stream);
   BT_CK(btsha1_launch_ragged(d_base, d_offsets, d_lens, 0, 0, n, d_digests, st));
   return 0;
 }
@@ -684,8 +748,7 @@ int bt_sha1_fill_synthetic(void *d_buf, uint64_t nbytes, uint64_t first_word, ui
   BT_CK(hipGetDevice(&dev));
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
-  hipStream_t st = pick_stream(stream, c);
-  if (!st) return -1;
+  hipStream_t st = pick_stream(stream);
   BT_CK(btsha1_launch_fill(d_buf, nbytes, first_word, seed, st));
   return 0;
 }
@@ -720,8 +783,7 @@ int bt_sha1_lookup_dev(const uint8_t *d_table, uint64_t n_table, const uint8_t *
   BT_CK(hipGetDevice(&dev));
   DevCtx *c = ctx_for(dev);
   if (!c) return -1;
-  hipStream_t st = pick_stream(stream, c);
-  if (!st) return -1;
+  hipStream_t st = pick_stream(stream);
   uint32_t cap = 1024;
   while (cap < 2 * n_table) cap <<= 1;  // load factor <= 1/2
   void *slots = nullptr;
@@ -740,42 +802,77 @@ int64_t bt_sha1_chunks_host(const void *h_in, uint64_t total_len, uint64_t chunk
   return chunks_host_on(t_dev, (const uint8_t *)h_in, total_len, chunk_len, h_digests);
 }
 
-int64_t bt_sha1_chunks_host_multi(const void *h_in, uint64_t total_len, uint64_t chunk_len, uint8_t *h_digests,
-                                  int ndev) {
-  if (chunk_len == 0) {
-    set_err("chunk_len must be > 0");
+int64_t bt_sha1_chunks_host_devices(const void *h_in, uint64_t total_len, uint64_t chunk_len, uint8_t *h_digests,
+                                    const int *devs, int nworkers) {
+  if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
+    set_err("chunk_len must be in [1, 4 GiB)");
+    return -1;
+  }
+  if (nworkers <= 0 || !devs) {
+    set_err("empty device list");
     return -1;
   }
   if (total_len == 0) return 0;
+  if (!h_in || !h_digests) {
+    set_err("null pointer");
+    return -1;
+  }
+  const int avail = device_count();
+  if (avail <= 0) {
+    set_err("no HIP device visible");
+    return -1;
+  }
+  for (int g = 0; g < nworkers; ++g)
+    if (devs[g] < 0 || devs[g] >= avail) {
+      set_err("device %d out of range (%d visible)", devs[g], avail);
+      return -1;
+    }
+  const uint64_t n = (total_len + chunk_len - 1) / chunk_len;
+  // Contiguous block split of the chunk index: worker g gets
+  // [g*n/G, (g+1)*n/G) -- possibly empty when G > n; only the globally last
+  // chunk can be short.  One host thread per worker; a device listed k times
+  // gets k independent contexts (streams + staging lanes), so the split,
+  // staging and ordered gather run exactly as on k distinct GPUs.
+  std::vector<int64_t> rc(nworkers, 0);
+  std::vector<std::string> errs(nworkers);
+  std::vector<int> repeat(nworkers, 0);
+  for (int g = 0; g < nworkers; ++g)
+    for (int h = 0; h < g; ++h) repeat[g] += devs[h] == devs[g];
+  std::vector<std::thread> th;
+  for (int g = 0; g < nworkers; ++g) {
+    th.emplace_back([&, g] {
+      const uint64_t lo = n * g / nworkers, hi = n * (g + 1) / nworkers;
+      if (lo == hi) return;
+      const uint64_t off = lo * chunk_len;
+      const uint64_t bytes = std::min<uint64_t>(hi * chunk_len, total_len) - off;
+      rc[g] = chunks_host_on(devs[g], (const uint8_t *)h_in + off, bytes, chunk_len, h_digests + 20 * lo, repeat[g]);
+      if (rc[g] >= 0 && (uint64_t)rc[g] != hi - lo) {
+        rc[g] = -1;
+        t_err = "short digest count";
+      }
+      errs[g] = t_err;
+    });
+  }
+  for (auto &t : th) t.join();
+  for (int g = 0; g < nworkers; ++g)
+    if (rc[g] < 0) {
+      t_err = "worker " + std::to_string(g) + " (device " + std::to_string(devs[g]) + "): " + errs[g];
+      return -1;
+    }
+  return (int64_t)n;
+}
+
+int64_t bt_sha1_chunks_host_multi(const void *h_in, uint64_t total_len, uint64_t chunk_len, uint8_t *h_digests,
+                                  int ndev) {
   const int avail = device_count();
   if (avail <= 0) {
     set_err("no HIP device visible");
     return -1;
   }
   if (ndev <= 0 || ndev > avail) ndev = avail;
-  const uint64_t n = (total_len + chunk_len - 1) / chunk_len;
-  if ((uint64_t)ndev > n) ndev = (int)n;
-  // Contiguous block split of the chunk index: device g gets
-  // [g*n/G, (g+1)*n/G); only the globally last chunk can be short.
-  std::vector<int64_t> rc(ndev, 0);
-  std::vector<std::string> errs(ndev);
-  std::vector<std::thread> th;
-  for (int g = 0; g < ndev; ++g) {
-    th.emplace_back([&, g] {
-      const uint64_t lo = n * g / ndev, hi = n * (g + 1) / ndev;
-      const uint64_t off = lo * chunk_len;
-      const uint64_t bytes = std::min<uint64_t>(hi * chunk_len, total_len) - off;
-      rc[g] = chunks_host_on(g, (const uint8_t *)h_in + off, bytes, chunk_len, h_digests + 20 * lo);
-      errs[g] = t_err;
-    });
-  }
-  for (auto &t : th) t.join();
-  for (int g = 0; g < ndev; ++g)
-    if (rc[g] < 0) {
-      t_err = "device " + std::to_string(g) + ": " + errs[g];
-      return -1;
-    }
-  return (int64_t)n;
+  std::vector<int> devs(ndev);
+  for (int g = 0; g < ndev; ++g) devs[g] = g;
+  return bt_sha1_chunks_host_devices(h_in, total_len, chunk_len, h_digests, devs.data(), ndev);
 }
 
 int64_t bt_sha1_chunks_file(void *fp, uint64_t chunk_len, uint8_t *h_digests, uint64_t max_chunks) {

@@ -13,8 +13,8 @@
 //                   line offset rides in the scalar soffset -> zero VALU
 //                   address arithmetic in the loop.
 //   k_sha1_lds      the hot path with coalesced LDS-DMA staging (a variant).
-//   k_sha1_lat      small fixed-layout batches (<= 16384 chunks: shahash,
-//                   small verify batches): a loader/schedule wave and a round
+//   k_sha1_lat      small fixed-layout batches (<= 64 chunks per CU, 16384 on
+//                   MI355X: shahash, small verify batches): a loader/schedule wave and a round
 //                   wave per 64 chunks meet in LDS, cutting a lone chain's
 //                   instruction count from 597 to ~426 per block.
 //   k_sha1_ragged   arbitrary (offset, length) messages and layouts the
@@ -125,10 +125,28 @@ __device__ __forceinline__ void epilogue(State &st, __amdgpu_buffer_rsrc_t rsrc,
 // last fread of make_chunks, chunk.c:20); the first wave past the full ones
 // (chunk0 = n_chunks rounded up to 64) hashes it alone, inside the same launch,
 // so its chain runs beside the full chunks' instead of after them.
-template <int NBUF, int L, int AUX, bool VERIFY>
+// In-kernel clock stamp (MI355X_MICROARCH.md "DVFS give-back" item 6): the
+// shader-clock counter and the constant-rate real-time counter, each read with
+// its lgkmcnt wait inside one asm statement, fenced against code motion.
+struct Stamp {
+  uint64_t mem, real;
+};
+__device__ __forceinline__ Stamp take_stamp() {
+  Stamp t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t.mem), "=s"(t.real)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+// STAMP (diagnostic build only, btsha1_launch_fixed_stamped): lane 0 of each
+// wave stores {memtime, realtime} before and after the main loop to
+// stamps[4*wave ..] through ordinary vector stores.  The production kernel is
+// the STAMP = false instantiation, in which no stamp executes.
+template <int NBUF, int L, int AUX, bool VERIFY, bool STAMP = false>
 __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_sha1_fixed(
     const uint8_t *__restrict__ base, uint64_t n_chunks, uint32_t pitch, uint32_t len, uint8_t *__restrict__ digests,
-    const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok, uint32_t tail_len) {
+    const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok, uint32_t tail_len, uint64_t *__restrict__ stamps) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint64_t chunk0 = (uint64_t)blockIdx.x * blockDim.x + (uint64_t)wave * 64u;  // wave-uniform
@@ -157,6 +175,8 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
   const uint32_t nslots = nblocks / (2u * L);
   const uint32_t nmain = (nslots / NBUF) * NBUF;  // slots covered by the pipelined loop
 
+  Stamp t0{};
+  if constexpr (STAMP) t0 = take_stamp();
   if (nmain) {
     u32x4 ring[NBUF][8 * L];
 #pragma unroll
@@ -173,6 +193,16 @@ __global__ __launch_bounds__(kBlock, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
         __builtin_amdgcn_sched_barrier(0);
         compress_slot<L>(st, ring[s]);
       }
+    }
+  }
+  if constexpr (STAMP) {
+    const Stamp t1 = take_stamp();
+    if (lane == 0) {
+      uint64_t *o = stamps + 4 * (chunk0 >> 6);
+      o[0] = t0.mem;
+      o[1] = t0.real;
+      o[2] = t1.mem;
+      o[3] = t1.real;
     }
   }
   epilogue<VERIFY>(st, rsrc, voff, nmain * 2u * L, len, lane, nvalid, chunk0, digests, expected, ok);
@@ -350,11 +380,34 @@ __device__ __forceinline__ void produce_wk(uint32_t (&w)[16], u32x4 *slot, uint3
   }
 }
 
+// Barrier accounting of k_sha1_lat.  S and R run different code, so the
+// workgroup barrier is met from different call sites; s_barrier counts WAVES,
+// and the kernel is correct only while both waves execute exactly the same
+// number of barriers: nb_total + 1 each (S: one per produced block + one
+// final; R: one before its loop + one per consumed block).  Any edit that
+// changes one side's block count deadlocks the workgroup silently.  Build
+// with -DBT_SHA1_DEBUG_BARRIERS to count them per wave and trap on a mismatch.
+#ifdef BT_SHA1_DEBUG_BARRIERS
+#define BT_LAT_BARRIER(cnt) \
+  do {                      \
+    ++(cnt);                \
+    __syncthreads();        \
+  } while (0)
+#define BT_LAT_CHECK(cnt, want) \
+  do {                          \
+    if ((cnt) != (want)) __builtin_trap(); \
+  } while (0)
+#else
+#define BT_LAT_BARRIER(cnt) __syncthreads()
+#define BT_LAT_CHECK(cnt, want) ((void)0)
+#endif
+
 // One block through S into slot p, then the block's barrier.
-__device__ __forceinline__ void produce_block(uint32_t (&w)[16], u32x4 (*lds)[20 * 64], uint32_t &p, uint32_t lane) {
+__device__ __forceinline__ void produce_block(uint32_t (&w)[16], u32x4 (*lds)[20 * 64], uint32_t &p, uint32_t lane,
+                                              uint32_t &nbar) {
   produce_wk<0, 80>(w, lds[p], lane);
   p ^= 1u;
-  __syncthreads();
+  BT_LAT_BARRIER(nbar);
 }
 
 template <bool VERIFY>
@@ -377,7 +430,11 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
     len = tail_len;
   }
   const uint32_t nblocks = len >> 6, r = len & 63u;
-  const uint32_t nb_total = nblocks + (r >= 56u ? 2u : 1u);  // + MD padding block(s)
+  // + MD padding block(s).  Both waves execute nb_total + 1 barriers (see
+  // "Barrier accounting" above).
+  const uint32_t nb_total = nblocks + (r >= 56u ? 2u : 1u);
+  uint32_t nbar = 0;
+  (void)nbar;
   if (wave == 0) {
     // ---- S: loads, schedule + K --------------------------------------------
     const uint32_t mine = lane < nvalid ? lane : nvalid - 1u;
@@ -405,7 +462,7 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
         if (b + k < nblocks) {  // wave-uniform
           uint32_t w[16];
           block_from_le(w, ring[k][0], ring[k][1], ring[k][2], ring[k][3]);
-          produce_block(w, lds, slot, lane);
+          produce_block(w, lds, slot, lane, nbar);
         }
       }
     }
@@ -417,29 +474,31 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
     for (int j = 0; j < 16; ++j) tail[j] |= (j == (int)wi) ? mark : 0u;
     const uint64_t bits = (uint64_t)len * 8ull;
     if (r >= 56u) {
-      produce_block(tail, lds, slot, lane);
+      produce_block(tail, lds, slot, lane, nbar);
 #pragma unroll
       for (int j = 0; j < 16; ++j) tail[j] = 0u;
     }
     tail[14] = (uint32_t)(bits >> 32);
     tail[15] = (uint32_t)bits;
-    produce_block(tail, lds, slot, lane);
-    __syncthreads();  // pairs with R's last barrier
+    produce_block(tail, lds, slot, lane, nbar);
+    BT_LAT_BARRIER(nbar);  // pairs with R's last barrier
+    BT_LAT_CHECK(nbar, nb_total + 1u);
   } else {
     // ---- R: rounds -----------------------------------------------------------
     State st;
     st.init();
-    __syncthreads();  // block 0 is in slot 0
+    BT_LAT_BARRIER(nbar);  // block 0 is in slot 0
     for (uint32_t b = 0; b < nb_total; ++b) {
       uint32_t a = st.h0, bb = st.h1, c = st.h2, d = st.h3, e = st.h4;
       consume_wk<0, 80>(a, bb, c, d, e, lds[b & 1u], lane);
-      __syncthreads();
+      BT_LAT_BARRIER(nbar);
       st.h0 += a;  // sha.c:446-450
       st.h1 += bb;
       st.h2 += c;
       st.h3 += d;
       st.h4 += e;
     }
+    BT_LAT_CHECK(nbar, nb_total + 1u);
     store_digest<VERIFY>(st, lane, nvalid, chunk0, digests, expected, ok);
   }
 }
@@ -651,22 +710,43 @@ __global__ __launch_bounds__(kBlock) void k_lookup_query(const uint8_t *__restri
 // ---------------------------------------------------------------------------
 using namespace btsha1;
 
+// Compute units of the current device, cached per device id.
+uint32_t btsha1_device_cus() {
+  static uint32_t cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  uint32_t v = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+  if (!v) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    v = (uint32_t)cus;
+    __atomic_store_n(&cache[dev], v, __ATOMIC_RELAXED);
+  }
+  return v;
+}
+
+// Below one wave per SIMD (CUs x 4 SIMDs x 64 lanes; 65536 chunks on a full
+// MI355X) use one-wave workgroups so the dispatcher spreads the waves over
+// distinct CUs instead of stacking four per CU: a chunk's latency is its
+// serial 8193-block chain, so a lone wave per SIMD finishes the batch soonest.
+static uint32_t chain_workgroup(uint64_t n) { return n < (uint64_t)btsha1_device_cus() * 4u * 64u ? 64u : (uint32_t)kBlock; }
+
 template <int NBUF, int L, int AUX>
 static hipError_t launch_fixed_v(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
-                                 const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, uint32_t tail_len) {
-  // Below one wave per SIMD (256 CUs x 4 SIMDs x 64 lanes) use one-wave
-  // workgroups so the dispatcher spreads the waves over distinct CUs instead
-  // of stacking four per CU: a chunk's latency is its serial 8193-block chain,
-  // so a lone wave per SIMD finishes the batch soonest.
-  const uint32_t wg = n < 65536 ? 64u : (uint32_t)kBlock;
+                                 const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, uint32_t tail_len,
+                                 uint64_t *d_stamps = nullptr) {
+  const uint32_t wg = chain_workgroup(n);
   const uint64_t threads = tail_len ? ((n + 63) & ~(uint64_t)63) + 64 : n;  // + the tail wave
   const uint64_t grid = (threads + wg - 1) / wg;
-  if (d_ok)
+  if (d_stamps)
+    hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, false, true>), dim3((uint32_t)grid), dim3(wg), 0, s,
+                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok, 0u, d_stamps);
+  else if (d_ok)
     hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, true>), dim3((uint32_t)grid), dim3(wg), 0, s,
-                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok, tail_len);
+                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok, tail_len, nullptr);
   else
     hipLaunchKernelGGL((k_sha1_fixed<NBUF, L, AUX, false>), dim3((uint32_t)grid), dim3(wg), 0, s,
-                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok, tail_len);
+                       (const uint8_t *)d_in, n, pitch, len, d_dig, d_exp, d_ok, tail_len, nullptr);
   return hipGetLastError();
 }
 
@@ -695,9 +775,13 @@ static hipError_t launch_lat(const void *d_in, uint64_t n, uint32_t pitch, uint3
 }
 
 // Batches of at most this many chunks take the latency kernel (0: never).
-static uint64_t g_lat_max = BT_SHA1_LATENCY_BATCH_DEFAULT;
+static uint64_t g_lat_max = BT_SHA1_LATENCY_AUTO;
 void btsha1_set_latency_batch(uint64_t max_chunks) { __atomic_store_n(&g_lat_max, max_chunks, __ATOMIC_RELAXED); }
-uint64_t btsha1_latency_batch() { return __atomic_load_n(&g_lat_max, __ATOMIC_RELAXED); }
+uint64_t btsha1_latency_batch_setting() { return __atomic_load_n(&g_lat_max, __ATOMIC_RELAXED); }
+uint64_t btsha1_latency_batch() {
+  const uint64_t v = btsha1_latency_batch_setting();
+  return v == BT_SHA1_LATENCY_AUTO ? (uint64_t)btsha1_device_cus() * 64u : v;
+}
 
 constexpr int kLdsVariant = 1010;  // bt_sha1_set_variant(10, 1, 0): LDS-staged k_sha1_lds
 constexpr int kLdsNtVariant = 1011;  // bt_sha1_set_variant(10, 1, 1): the same with nt DMA loads
@@ -738,12 +822,31 @@ hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uin
   return hipErrorInvalidValue;
 }
 
+hipError_t btsha1_launch_fixed_stamped(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
+                                       uint64_t *d_stamps, hipStream_t s, int variant) {
+  if (n == 0) return hipSuccess;
+  if (!d_stamps) return hipErrorInvalidValue;
+#define BT_CASE(N, L, A) \
+  if (variant == N * 100 + L * 10 + (A ? 1 : 0)) \
+    return launch_fixed_v<N, L, A>(d_in, n, pitch, len, d_dig, nullptr, nullptr, s, 0u, d_stamps);
+  BT_FIXED_VARIANTS(BT_CASE)
+#undef BT_CASE
+  return hipErrorInvalidValue;  // the LDS variant has no stamped build
+}
+
+const char *btsha1_fixed_kernel_name(uint64_t n, int variant) {
+  if (n == 0) return "none";
+  if (n <= btsha1_latency_batch()) return "k_sha1_lat";
+  if (variant == kLdsVariant || variant == kLdsNtVariant) return "k_sha1_lds";
+  return "k_sha1_fixed";
+}
+
 hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t pitch,
                                 uint32_t fixed_len, uint64_t n, uint8_t *d_dig, hipStream_t s) {
   if (n == 0) return hipSuccess;
   // As launch_fixed_v: below one wave per SIMD, one-wave workgroups spread
   // the chains over CUs (each message is a serial chain).
-  const uint32_t wg = n < 65536 ? 64u : (uint32_t)kBlock;
+  const uint32_t wg = chain_workgroup(n);
   const uint64_t grid = (n + wg - 1) / wg;
   hipLaunchKernelGGL(k_sha1_ragged, dim3((uint32_t)grid), dim3(wg), 0, s, (const uint8_t *)d_base, d_off,
                      d_len, pitch, fixed_len, n, d_dig);

@@ -12,11 +12,25 @@
 hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
                                const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant,
                                uint32_t tail_len = 0);
+// Diagnostic build of the hot kernel (variant as above, no verify, no tail):
+// lane 0 of every wave writes {s_memtime, s_memrealtime} at the start of its
+// loop and after it to d_stamps[4*wave ..] (4 u64 per wave of 64 chunks).
+hipError_t btsha1_launch_fixed_stamped(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
+                                       uint64_t *d_stamps, hipStream_t s, int variant);
+// Name of the kernel btsha1_launch_fixed runs for a batch of n chunks (tail
+// included) on the current device with this variant.
+const char *btsha1_fixed_kernel_name(uint64_t n, int variant);
 // Batches of at most max_chunks chunks (tail included) take the latency kernel
-// k_sha1_lat instead of the selected variant; 0 disables it.
-#define BT_SHA1_LATENCY_BATCH_DEFAULT 16384
+// k_sha1_lat instead of the selected variant; 0 disables it.  The default,
+// BT_SHA1_LATENCY_AUTO, is 64 chunks per CU of the launching device (one
+// two-wave workgroup per CU: past that the latency kernel's S and R waves
+// start sharing SIMDs and it loses to the hot kernel).
+#define BT_SHA1_LATENCY_AUTO UINT64_MAX
 void btsha1_set_latency_batch(uint64_t max_chunks);
-uint64_t btsha1_latency_batch();
+uint64_t btsha1_latency_batch_setting();  // raw setting (may be BT_SHA1_LATENCY_AUTO)
+uint64_t btsha1_latency_batch();          // effective threshold on the current device
+// Compute units of the current device (cached per device; 256 on MI355X).
+uint32_t btsha1_device_cus();
 // Hot-kernel variant code = ring slots*100 + lines per slot*10 + nt flag.
 bool btsha1_fixed_variant_ok(int code);
 // n messages at d_base + d_off[i], d_len[i] bytes each; with d_off == NULL,

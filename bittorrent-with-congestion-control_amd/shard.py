@@ -1,4 +1,5 @@
-"""shard.py -- how a chunk batch is split over GPUs.
+"""shard.py -- how a chunk batch is split over GPUs, and the
+rank logic bench.py runs on every rank.
 
 Chunks are independent (chunk.c:20-21 carries no state between chunks), so
 the multi-GPU path is an embarrassingly parallel split with no data-path
@@ -6,11 +7,13 @@ collective:
   * weak scaling (bench.py, BASELINE config 4): every rank owns a fixed count
     of chunks, global indices [rank*C, (rank+1)*C), and generates / hashes
     them in its own HBM;
-  * strong split of one image (bt_sha1_chunks_host_multi in the C library):
-    device g of G takes [g*n//G, (g+1)*n//G) -- identical formula.
-The only cross-rank traffic is a host-side gather of the 20-byte digests,
-done over a CPU (gloo) group after the timed region.
+  * strong split of one image (bt_sha1_chunks_host_devices in the C library):
+    worker g of G takes [g*n//G, (g+1)*n//G) -- identical formula.
+Ranks meet only on a CPU (gloo) group: the timing barriers, the
+max-over-ranks reduction of the wall times, and a host-side gather of the
+20-byte digests after the timed region.  No RCCL collective is involved.
 """
+import time
 
 
 def weak_range(rank, chunks_per_rank):
@@ -22,6 +25,24 @@ def weak_range(rank, chunks_per_rank):
 def block_range(n, world, rank):
     """Contiguous block split of n chunks (same formula as the C library)."""
     return n * rank // world, n * (rank + 1) // world
+
+
+def barrier(world, group=None):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier(group=group)
+
+
+def gather_floats(values, world, group=None):
+    """Every rank's list of floats, in rank order (all ranks get all)."""
+    if world == 1:
+        return [list(values)]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(list(values), dtype=torch.float64)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    return [[float(x) for x in p] for p in parts]
 
 
 def gather_digests(local: bytes, world, rank, group=None):
@@ -36,11 +57,44 @@ def gather_digests(local: bytes, world, rank, group=None):
     sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
     cap = int(max(s.item() for s in sizes))
-    buf = torch.zeros(cap, dtype=torch.uint8)
+    buf = torch.zeros(max(cap, 1), dtype=torch.uint8)
     if local:
         buf[:len(local)] = torch.frombuffer(bytearray(local), dtype=torch.uint8)
-    parts = [torch.zeros(cap, dtype=torch.uint8) for _ in range(world)] if rank == 0 else None
+    parts = [torch.zeros(max(cap, 1), dtype=torch.uint8) for _ in range(world)] if rank == 0 else None
     dist.gather(buf, parts, dst=0, group=group)
     if rank != 0:
         return None
     return b"".join(bytes(p[:int(s.item())].numpy().tobytes()) for p, s in zip(parts, sizes))
+
+
+def run_rank(hasher, steps, warmup, world, rank, group=None):
+    """The per-rank benchmark protocol of bench.py (the driver's contract):
+    `warmup` untimed steps; barrier + sync; `steps` timed steps; sync +
+    barrier; then the max over ranks of the wall time and of the hot kernel's
+    average time, and the digests gathered to rank 0 in global chunk order.
+
+    `hasher` provides step(i) (launch one pass over the rank's chunks),
+    sync() (wait for the device), kernel_ms() (the hot kernel's average launch
+    time over the timed steps, or None) and digests() (the rank's digests,
+    bytes).  bench.py passes the HIP hasher; tests pass a CPU stub.
+    Returns a dict on every rank ('digests' only on rank 0)."""
+    for i in range(warmup):
+        hasher.step(-1 - i)
+    hasher.sync()
+    barrier(world, group)
+    hasher.sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        hasher.step(i)
+    hasher.sync()
+    barrier(world, group)
+    wall = time.perf_counter() - t0
+    kern = hasher.kernel_ms()
+    per_rank = gather_floats([wall, -1.0 if kern is None else kern], world, group)
+    digests = gather_digests(hasher.digests(), world, rank, group)
+    return {
+        "wall_max": max(w for w, _ in per_rank),
+        "kernel_ms_max": max(k for _, k in per_rank) if kern is not None else None,
+        "per_rank": per_rank,
+        "digests": digests,
+    }

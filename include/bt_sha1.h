@@ -19,7 +19,9 @@
  * synthetic generator used by the bench and the tests.
  *
  * Conventions: plain pointers and sizes; `stream` is a hipStream_t passed as
- * void* (NULL = the library's own stream for the current device); device
+ * void* (NULL = the current device's null/default stream, so a call is
+ * ordered with the caller's default-stream work, e.g. torch's default stream,
+ * exactly like a kernel the caller launches on stream 0); device
  * pointers are prefixed d_, host pointers h_.  Return 0 (or a count) on
  * success, -1 on error.
  */
@@ -44,8 +46,13 @@ int bt_sha1_device_count(void);
 int bt_sha1_set_device(int device);
 /* Human-readable description of the last error on this thread. */
 const char *bt_sha1_last_error(void);
-/* Library / kernel build description (arch, ring depth). */
+/* Library / kernel build description (arch, ring depth, latency threshold,
+ * source id). */
 const char *bt_sha1_build_info(void);
+/* Id of the kernel sources this library was compiled from (first 16 hex
+ * digits of the SHA-256 of sha1_kernels.hip + sha1_device.h): ties profiles
+ * (PMC traffic, rocprof summaries) to the build that produced them. */
+const char *bt_sha1_source_id(void);
 /* Hot-kernel register-ring depth in 128-byte lines (2, 3 or 4; default 3).
  * 10 selects the LDS-staged variant (coalesced loads DMA'd into LDS). */
 int bt_sha1_set_ring_depth(int nbuf);
@@ -55,8 +62,25 @@ int bt_sha1_set_variant(int nbuf, int lines, int nt);
 /* Batches of at most max_chunks chunks take the latency kernel (a loader /
  * schedule wave and a round wave per 64 chunks, meeting in LDS), which
  * shortens a lone chunk's serial chain; larger batches take the hot-kernel
- * variant above.  0 disables it; default 16384.  Returns the previous value. */
+ * variant above.  0 disables it; UINT64_MAX (the default) = 64 chunks per
+ * compute unit of the launching device (16384 on a full MI355X).  Returns the
+ * previous setting. */
 uint64_t bt_sha1_set_latency_batch(uint64_t max_chunks);
+/* Name of the kernel a fixed-layout batch of n_chunks chunks runs on the
+ * current device ("k_sha1_fixed", "k_sha1_lat" or "k_sha1_lds"); NULL without
+ * a device. */
+const char *bt_sha1_kernel_name(uint64_t n_chunks);
+/* Diagnostic (bench clock measurement): hashes the batch like
+ * bt_sha1_chunks_dev through a separately compiled build of the hot kernel
+ * whose lane 0 of every wave stores {s_memtime, s_memrealtime} before and
+ * after its main loop into d_stamps[4*w .. 4*w+3] (w = chunk index / 64;
+ * d_stamps holds 4*ceil(n/64) uint64).  The in-kernel shader clock is
+ * delta(memtime) / delta(realtime) * bt_sha1_wallclock_khz().  The production
+ * kernel executes no stamp. */
+int bt_sha1_clock_probe(const void *d_in, uint64_t n, uint64_t chunk_len, uint64_t pitch, uint8_t *d_digests,
+                        uint64_t *d_stamps, void *stream);
+/* Rate of s_memrealtime on the current device in kHz (100000 on MI355X). */
+int64_t bt_sha1_wallclock_khz(void);
 
 /* ---- device-resident batches (the hot path) ---------------------------- */
 /* n chunks of chunk_len bytes, chunk i at d_in + i*pitch (pitch >= chunk_len).
@@ -90,6 +114,13 @@ int64_t bt_sha1_chunks_host(const void *h_in, uint64_t total_len, uint64_t chunk
  * device, contiguous chunk ranges, digests gathered into h_digests in order. */
 int64_t bt_sha1_chunks_host_multi(const void *h_in, uint64_t total_len, uint64_t chunk_len,
                                   uint8_t *h_digests, int ndev);
+/* The same split over an explicit list of nworkers device ids (SURVEY.md §8e:
+ * worker g takes chunks [g*n/G, (g+1)*n/G)).  An id may repeat: each repeat
+ * is an independent worker (own host thread, streams and staging) on that
+ * device, so the multi-GPU split / staging / ordered gather can be run with
+ * any worker count on one GPU.  Returns the chunk count. */
+int64_t bt_sha1_chunks_host_devices(const void *h_in, uint64_t total_len, uint64_t chunk_len,
+                                    uint8_t *h_digests, const int *devs, int nworkers);
 /* make_chunks over a FILE* with an explicit chunk size (make_chunks uses
  * BT_CHUNK_SIZE).  h_digests must hold 20*ceil(size/chunk_len) bytes. */
 int64_t bt_sha1_chunks_file(void *fp /* FILE* */, uint64_t chunk_len, uint8_t *h_digests,

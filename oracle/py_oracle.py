@@ -111,6 +111,22 @@ def compress_blocks(state, blocks: bytes):
     return list(st)
 
 
+ORACLE_SO_O0 = os.path.join(HERE, "liboracle_sha1_O0.so")
+
+
+def load_port(opt="O2"):
+    """Our restatement as a shahash-compatible library: or_shahash(buf, len, out)
+    (-O2 build, or the -O0 one matching the reference Makefile's flags)."""
+    if opt == "O2":
+        return _lib
+    if not os.path.exists(ORACLE_SO_O0):
+        return None
+    lib = ctypes.CDLL(ORACLE_SO_O0)
+    lib.or_shahash.argtypes = [_vp, ctypes.c_int, _vp]
+    lib.or_shahash.restype = None
+    return lib
+
+
 def load_reference(opt="O2"):
     """The reference's shahash from oracle/_ref (None when not built here)."""
     path = REF_SO if opt == "O2" else REF_SO_O0

@@ -370,6 +370,34 @@ def test_reference_make_chunks_linked_to_dropin(tmp_path):
     assert out == open(os.path.join(GOLDEN, "C.tar.make-chunks.out")).read()
 
 
+def test_reference_save_chunk_linked_to_dropin(tmp_path):
+    """Caller #2 at the boundary: the reference peer's own util.c (save_data_packet
+    util.c:250-277 + save_chunk util.c:304-337) and file.c, compiled unmodified
+    and linked against libbtsha1.so in place of chunk.o + sha.o (reference
+    Makefile:6), receive C.tar's four chunks as 1484-byte DATA payloads; chunk
+    2 arrives corrupted first.  Exactly one "Verification failed!", the failed
+    chunk goes back to NOT_STARTED (common.h: 2), every chunk ends OWNED (0)
+    and the written file is C.tar byte for byte (util.c:322-323)."""
+    exe = os.path.join(REPO, "oracle", "_ref", "save-chunk-dropin")
+    assert os.path.exists(exe), "built by `make dropin` in the build container (needs the reference sources)"
+    data = tmp_path / "C.tar"
+    data.write_bytes(c_tar_bytes())
+    has = tmp_path / "has.chunks"
+    has.write_text("")
+    out = tmp_path / "out.tar"
+    env = dict(os.environ, LD_LIBRARY_PATH=PKG + ":" + os.environ.get("LD_LIBRARY_PATH", ""))
+    r = subprocess.run([exe, "-c", "2", str(data), os.path.join(GOLDEN, "ref_C.chunks"),
+                        os.path.join(GOLDEN, "C.tar.make-chunks.out"), str(has), str(out)],
+                       capture_output=True, env=env, timeout=120)
+    text = r.stdout.decode()
+    assert r.returncode == 0, (text[-2000:], r.stderr.decode()[-2000:])
+    assert text.count("Verification failed!") == 1
+    states = [tuple(map(int, l.split()[1:])) for l in text.splitlines() if l.startswith("STATE ")]
+    assert states == [(0, 0), (1, 0), (2, 2), (2, 0), (3, 0)], states
+    assert "ALL_FINISHED 1" in text
+    assert out.read_bytes() == data.read_bytes()
+
+
 def test_verify_stream_cli(tmp_path):
     exe = os.path.join(PKG, "bin", "verify-stream")
     p = tmp_path / "C.tar"
@@ -632,3 +660,105 @@ def test_randomized_layouts_vs_oracle(bt, torch, oracle):
         for i in range(n):
             want = oracle.sha1(bytes(host[i * pitch:i * pitch + chunk_len]))
             assert raw[20 * i:20 * i + 20] == want, (case, chunk_len, pitch, n, in_off, out_off, i)
+
+
+# ---- multi-device split on one GPU (bt_sha1_chunks_host_devices) ------------------
+@pytest.mark.parametrize("workers", [2, 3, 8])
+def test_multi_device_split_with_repeated_device_ids(bt, oracle, workers):
+    """The multi-GPU host split (worker g takes chunks
+    [g*n/G, (g+1)*n/G), one host thread, streams and staging lanes per worker,
+    digests gathered in chunk order) run with `workers` workers on device 0.
+    Checked against the reference's make-chunks output for C.tar (4 full
+    chunks) and for the short-tail file (3 full chunks + 12345 B: the short
+    chunk lands on the last worker)."""
+    devs = [0] * workers
+    img = c_tar_bytes()
+    want_c = open(os.path.join(GOLDEN, "C.tar.make-chunks.out")).read()
+    got = bt.chunks_host(img, devs=devs)
+    assert "".join(f"{i} {d.hex()}\n" for i, d in enumerate(got)) == want_c
+    tail = bytes(oracle.fill_synthetic(3 * CHUNK + 12345, 0, oracle.SEED_TAIL))
+    want_t = open(os.path.join(GOLDEN, "tail.make-chunks.out")).read()
+    got = bt.chunks_host(tail, devs=devs)
+    assert "".join(f"{i} {d.hex()}\n" for i, d in enumerate(got)) == want_t
+    # more chunks than one batch per worker, small chunks, short last chunk
+    big = bytes(oracle.fill_synthetic(3 * 1024 * 1024 + 4097, 5, 11))
+    assert bt.chunks_host(big, chunk_len=4096, devs=devs) == oracle.hash_chunks(big, 4096)
+    # registered (pinned) image: every worker DMAs its own slice directly
+    import numpy as np
+    arr = np.frombuffer(bytearray(tail), dtype=np.uint8)
+    bt.host_register(arr.ctypes.data, arr.nbytes)
+    try:
+        raw = bt.chunks_host_addr(arr.ctypes.data, arr.nbytes, devs=devs)
+    finally:
+        bt.host_unregister(arr.ctypes.data)
+    assert "".join(f"{i} {raw[20 * i:20 * i + 20].hex()}\n" for i in range(len(raw) // 20)) == want_t
+
+
+def test_multi_device_split_rejects_bad_lists(bt):
+    with pytest.raises(bt.BtSha1Error, match="out of range"):
+        bt.chunks_host(b"x" * 100, 64, devs=[0, 99])
+    with pytest.raises(bt.BtSha1Error, match="empty"):
+        bt.chunks_host(b"x" * 100, 64, devs=[])
+
+
+# ---- NULL stream = the caller's default stream (ADVICE r01) --------------------------
+def test_null_stream_orders_after_default_stream_work(bt, torch, oracle):
+    """A device call with stream=None must see input written by the caller's
+    earlier default-stream kernels and must not race the caller's zeroing of
+    the output: torch's default stream has handle 0, and NULL means exactly
+    that stream.  The input is written at the end of a long default-stream
+    queue (a chain of matmuls), so an unordered launch would read zeros."""
+    assert torch.cuda.current_stream().cuda_stream == 0
+    n = 256
+    want = [bytes.fromhex(l.split()[1]) for l in open(os.path.join(GOLDEN, "synth4096.txt"))
+            if not l.startswith("#")][:n]
+    src = torch.empty(n * CHUNK, dtype=torch.uint8, device="cuda")
+    bt.fill_synthetic(src.data_ptr(), n * CHUNK, 0, oracle.SEED_SYNTH, None)
+    torch.cuda.synchronize()
+    for trial in range(3):
+        buf = torch.zeros(n * CHUNK, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        a = torch.randn(4096, 4096, device="cuda")
+        for _ in range(20):  # ~tens of ms of default-stream work ahead of the copy
+            a = a @ a
+            a = a / (a.abs().max() + 1)
+        buf.copy_(src)  # written only after the matmul chain
+        dig = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+        bt.chunks_dev(buf.data_ptr(), n, CHUNK, CHUNK, dig.data_ptr(), None)
+        dig2 = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+        bt.fill_synthetic(dig2.data_ptr(), 16, 0, 1, None)  # a NULL-stream write the caller then overwrites
+        dig2.zero_()
+        torch.cuda.synchronize()
+        assert digests_of(torch, dig, n) == want, trial
+        assert int(dig2.sum().item()) == 0, trial
+
+
+def test_kernel_name_reports_the_launch(bt):
+    lat = bt.set_latency_batch(2**64 - 1)  # auto
+    try:
+        assert bt.kernel_name(1) == "k_sha1_lat"
+        assert bt.kernel_name(16384) == "k_sha1_lat"  # 64 per CU on a 256-CU MI355X
+        assert bt.kernel_name(131072) == "k_sha1_fixed"
+        assert "latency_batch=auto" in bt.build_info()
+    finally:
+        bt.set_latency_batch(lat)
+
+
+def test_clock_probe_stamps_and_digests(bt, torch, oracle):
+    """The bench's clock probe hashes exactly like the production kernel and
+    leaves one sane stamp quadruple per wave."""
+    n = 4096
+    buf = torch.empty(n * CHUNK, dtype=torch.uint8, device="cuda")
+    bt.fill_synthetic(buf.data_ptr(), n * CHUNK, 0, oracle.SEED_SYNTH, None)
+    dig = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(4 * (n // 64), dtype=torch.int64, device="cuda")
+    bt.clock_probe(buf.data_ptr(), n, CHUNK, CHUNK, dig.data_ptr(), st.data_ptr(), None)
+    torch.cuda.synchronize()
+    want = [bytes.fromhex(l.split()[1]) for l in open(os.path.join(GOLDEN, "synth4096.txt"))
+            if not l.startswith("#")]
+    assert digests_of(torch, dig, n) == want
+    s = st.view(-1, 4).cpu()
+    dm, dr = (s[:, 2] - s[:, 0]).double(), (s[:, 3] - s[:, 1]).double()
+    assert bool((dm > 0).all()) and bool((dr > 0).all())
+    mhz = float((dm / dr).median()) * bt.wallclock_khz() / 1000.0
+    assert 500.0 < mhz < 3000.0, mhz

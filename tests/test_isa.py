@@ -37,6 +37,29 @@ def test_hot_loop_mix(asm, nbuf, lines):
     assert m["scratch_bytes"] == 0 and m["vgprs"] <= 256, m
 
 
+def test_clock_probe_build_runs_the_same_loop(asm):
+    """bench.py's clock probe (bt_sha1_clock_probe) times the STAMP build of the
+    hot kernel: its main loop must be the production loop, instruction for
+    instruction, so the clock it reads is the clock the benchmark runs at."""
+    mod, text = asm
+    prod = mod.loop_mix(text, 3, 1)
+    stamped = mod.loop_mix(text, 3, 1, stamp=True)
+    assert stamped["mix_per_block"] == prod["mix_per_block"], (stamped, prod)
+    body = text[text.index(mod.fixed_symbol(3, 1, True) + ":"):]
+    body = body[:body.index(".Lfunc_end")]
+    assert body.count("s_memtime") == 2 and body.count("s_memrealtime") == 2
+    prod_body = text[text.index(mod.fixed_symbol(3, 1) + ":"):]
+    assert "s_memtime" not in prod_body[:prod_body.index(".Lfunc_end")]
+
+
+def test_no_scalar_stores_anywhere(asm):
+    """No kernel writes through the scalar data cache (gpurun refuses such code)."""
+    import re
+    _, text = asm
+    assert not re.search(r"^\s*(s_store_dword|s_buffer_store|s_scratch_store|s_dcache_wb|s_dcache_discard|s_atomic)",
+                         text, re.M)
+
+
 def _rotl(x, n):
     return ((x << n) | (x >> (32 - n))) & 0xFFFFFFFF
 
@@ -56,8 +79,8 @@ def test_schedule_squared_twice_identity():
             assert w[t] == _rotl(w[t - 12] ^ w[t - 32] ^ w[t - 56] ^ w[t - 64], 4)
 
 
-def _first_wait_after_each_load_group(text, sym):
-    """For every run of 16-byte global loads in kernel `sym`, the vmcnt of the
+def _first_wait_after_each_load_group(text, sym, load="global_load_dwordx4"):
+    """For every run of 16-byte loads in kernel `sym`, the vmcnt of the
     first s_waitcnt that follows it."""
     import re
     body = text[text.index(sym + ":"):]
@@ -65,7 +88,7 @@ def _first_wait_after_each_load_group(text, sym):
     out, in_group = [], False
     for line in body.splitlines():
         line = line.strip()
-        if line.startswith("global_load_dwordx4"):
+        if line.startswith(load):
             in_group = True
             continue
         m = re.match(r"s_waitcnt vmcnt\((\d+)\)", line)
@@ -85,4 +108,50 @@ def test_ragged_ring_keeps_loads_in_flight(asm, sym):
     _, text = asm
     waits = _first_wait_after_each_load_group(text, sym)
     assert waits, "no 16-byte load groups found"
+    assert min(waits) >= 4, waits
+
+
+LAT_SYM = "_ZN6btsha110k_sha1_latILb0EEEvPKhmjjPhS2_S3_j"
+
+
+def _loops(text, sym):
+    """(header label, body text) of every innermost loop of kernel `sym`."""
+    import re
+    body = text[text.index(sym + ":"):]
+    body = body[:body.index(".Lfunc_end")]
+    out = []
+    for m in re.finditer(r"^(\.LBB\d+_\d+):[^\n]*Inner Loop Header", body, re.M):
+        label = m.group(1)
+        end = re.search(r"s_cbranch_\w+ " + re.escape(label) + r"\b", body[m.end():])
+        if end:  # loops entered by fall-through from a latch block are not innermost-simple
+            out.append((label, body[m.end():m.end() + end.start()]))
+    return out
+
+
+def test_latency_kernel_round_wave_structure(asm):
+    """k_sha1_lat: the round wave R's loop is one 64-byte block
+    per iteration with 5 VALU per round (+ the 5 state adds) = 405, its 80 W+K
+    words read as 20 ds_read_b128 from ONE 80-word LDS slot, and exactly one
+    s_barrier (the loader wave S pairs it with one barrier per block).  This
+    layout was once lost in a revert and caught only by re-timing."""
+    import collections
+    _, text = asm
+    r_loops = [b for _, b in _loops(text, LAT_SYM) if "ds_read_b128" in b and "buffer_load" not in b]
+    assert len(r_loops) == 1, len(r_loops)
+    ops = collections.Counter(l.strip().split()[0] for l in r_loops[0].splitlines()
+                              if l.strip() and not l.strip().startswith((".", ";")))
+    valu = sum(v for k, v in ops.items() if k.startswith("v_"))
+    assert valu == 405, ops
+    assert ops["ds_read_b128"] == 20 and ops["s_barrier"] == 1, ops
+    assert ops["v_alignbit_b32"] == 160 and ops["v_bitop3_b32"] == 80, ops
+
+
+def test_latency_kernel_loader_ring_keeps_loads_in_flight(asm):
+    """S's four-block register ring never waits for the block it just issued:
+    the first wait after each group of 16-byte buffer loads leaves >= 4 of them
+    outstanding (a vmcnt(0) there would put a memory round trip on every block
+    R waits for at the barrier)."""
+    _, text = asm
+    waits = _first_wait_after_each_load_group(text, LAT_SYM, load="buffer_load_dwordx4")
+    assert waits, "no buffer load groups found"
     assert min(waits) >= 4, waits

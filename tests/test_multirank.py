@@ -55,6 +55,78 @@ def _worker(rank, world, port, mode, q):
     dist.destroy_process_group()
 
 
+class StubHasher:
+    """CPU stand-in for bench.DeviceHasher (same protocol: step/sync/kernel_ms/
+    digests); the hashing is the oracle on small chunks."""
+
+    def __init__(self, oracle, first_chunk, chunks):
+        self.oracle, self.first, self.C = oracle, first_chunk, chunks
+        self.data = oracle.fill_synthetic(chunks * CHUNK, first_chunk * (CHUNK // 8), oracle.SEED_SYNTH)
+        self.steps, self.out = [], b""
+
+    def step(self, i):
+        self.steps.append(i)
+        self.out = b"".join(self.oracle.hash_chunks(self.data, CHUNK))
+
+    def sync(self):
+        pass
+
+    def kernel_ms(self):
+        return 1.0 + self.first / 1000.0  # distinct per rank: the max must pick the last rank
+
+    def digests(self):
+        return self.out
+
+
+def _bench_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import py_oracle
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shard = _load_shard()
+    C = 6
+    lo, _ = shard.weak_range(rank, C)
+    h = StubHasher(py_oracle, lo, C)
+    res = shard.run_rank(h, steps=4, warmup=2, world=world, rank=rank)
+    assert h.steps == [-1, -2, 0, 1, 2, 3]
+    if rank == 0:
+        q.put((res["digests"], res["kernel_ms_max"], len(res["per_rank"])))
+    else:
+        assert res["digests"] is None
+    shard.barrier(world)
+    dist.destroy_process_group()
+
+
+def test_bench_rank_protocol_two_ranks(oracle):
+    """bench.py's own per-rank protocol (shard.run_rank: warmup, barriers,
+    timed steps, max over ranks, ordered digest gather) at world size 2 with a
+    CPU stub hasher: rank 0 ends up with all 12 digests in global order."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    dig, kmax, nranks = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = b"".join(oracle.hash_chunks(oracle.fill_synthetic(12 * CHUNK, 0, oracle.SEED_SYNTH), CHUNK))
+    assert dig == want
+    assert nranks == 2 and abs(kmax - 1.006) < 1e-9
+
+
+def test_bench_uses_the_shard_protocol():
+    """The bench's rank split / timing / gather is shard.py's (covered above),
+    not an inline copy."""
+    src = open(os.path.join(REPO, "bench.py")).read()
+    assert "shard.run_rank(" in src and "shard.weak_range(" in src
+    assert "dist.gather(" not in src and "dist.all_gather(" not in src
+
+
 @pytest.mark.parametrize("mode", ["weak", "strong"])
 def test_two_rank_split_equals_single(mode, oracle):
     world = 2

@@ -33,16 +33,19 @@ for step in "$@"; do
   case $step in
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    tests_new) run pytest_gpu_new 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+      -k "multi_device or null_stream or kernel_name or clock_probe or save_chunk" ;;
     bench) run bench 600 python3 bench.py ;;
     bench_rings)
       for r in 2 3 4; do run bench_ring$r 300 python3 bench.py --ring $r --steps 10 --no-cpu-baseline; done ;;
     prof)
+      # same process: the bench line (prof.log) and the rocprof kernel stats
       mkdir -p "$OUT/prof"
       run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench \
-        -- python3 "$ROOT/bench.py" --steps 10 --no-cpu-baseline ;;
+        -- python3 "$ROOT/bench.py" --steps 20 --no-cpu-baseline --no-host-path --no-clock ;;
     pmc)
       mkdir -p "$OUT/pmc"
-      PB="python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+      PB="python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-path --no-clock"
       run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o fetch -- $PB
       run pmc_rdreq 600 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc" -o rdreq -- $PB
       run pmc_valu 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc" -o valu -- $PB

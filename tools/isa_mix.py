@@ -30,8 +30,13 @@ def compile_asm(out):
                    check=True, capture_output=True)
 
 
-def loop_mix(asm_text, nbuf, lines):
-    sym = f"_ZN6btsha112k_sha1_fixedILi{nbuf}ELi{lines}ELi0ELb0EEEvPKhmjjPhS2_S3_j"
+def fixed_symbol(nbuf, lines, stamp=False):
+    """Mangled name of k_sha1_fixed<nbuf, lines, 0, false, stamp>."""
+    return f"_ZN6btsha112k_sha1_fixedILi{nbuf}ELi{lines}ELi0ELb0ELb{int(stamp)}EEEvPKhmjjPhS2_S3_jPm"
+
+
+def loop_mix(asm_text, nbuf, lines, stamp=False):
+    sym = fixed_symbol(nbuf, lines, stamp)
     start = asm_text.index(sym + ":")
     body = asm_text[start:]
     end_fn = body.index(".Lfunc_end")
@@ -51,7 +56,7 @@ def loop_mix(asm_text, nbuf, lines):
     per_block = {k: v / blocks for k, v in sorted(ops.items())}
     total = sum(per_block.values())
     half = sum(v for k, v in per_block.items() if k in HALF_RATE)
-    return {"kernel": f"k_sha1_fixed<{nbuf},{lines},0,false>", "blocks_per_iteration": blocks,
+    return {"kernel": f"k_sha1_fixed<{nbuf},{lines},0,false,{str(stamp).lower()}>", "blocks_per_iteration": blocks,
             "valu_per_block": total, "half_rate_per_block": half, "full_rate_per_block": total - half,
             "mix_per_block": per_block, "vgprs": vgprs, "scratch_bytes": scratch}
 

@@ -20,7 +20,7 @@ import statistics
 import sys
 from collections import defaultdict
 
-HOT = "k_sha1_fixed"
+HOT = "k_sha1_fixed<3, 1, 0, false, false>"  # the production instantiation (not the stamped probe build)
 
 
 def counters(path):
@@ -55,6 +55,15 @@ def main():
             for k, v in cs.items():
                 agg[k].append(v)
             durs.append((meta[d][1] - meta[d][0]) * 1e-6)
+    # The bench line printed by the profiled process itself (gpu_session `prof`).
+    bench_line = None
+    pl = os.path.join(src, "prof.log")
+    if os.path.exists(pl):
+        for l in open(pl):
+            if l.startswith("{") and '"metric"' in l:
+                bench_line = json.loads(l)
+    if bench_line:
+        json.dump(bench_line, open(os.path.join(out, "bench_line_same_process.json"), "w"), indent=1)
     summary = {k: statistics.mean(v) for k, v in agg.items()}
     summary["profiled_dispatches"] = len(durs)
     summary["profiled_kernel_ms_mean"] = statistics.mean(durs) if durs else None
@@ -67,7 +76,11 @@ def main():
     json.dump(summary, open(os.path.join(out, "pmc_summary.json"), "w"), indent=1)
     if traffic:
         hbm = traffic.get("fetch_size_bytes_corrected", traffic.get("rdreq_bytes"))
+        build = (bench_line or {}).get("config", {}).get("build", "")
         tj = {"chunks": chunks, "pitch": 512 * 1024, "hbm_bytes_per_launch": hbm,
+              "source_id": build.split("src=")[1].split()[0] if "src=" in build else None,
+              "variant": build.split("ring=")[1].split()[0] if "ring=" in build else None,
+              "kernel": "k_sha1_fixed",
               "algorithmic_bytes_per_launch": algo, "ratio": hbm / algo, **traffic,
               "method": "rocprofv3 --pmc FETCH_SIZE (x1024 KiB, x2 gfx950 half-count) and TCC_EA0_RDREQ_sum x128 B, "
                         "separate passes, hot kernel dispatches averaged"}
@@ -75,10 +88,22 @@ def main():
     lines = [f"# Profile summary {rnd}", "", f"hot kernel `{HOT}`, {chunks} x 512 KiB chunks per launch", ""]
     if os.path.exists(stats):
         lines += ["## rocprofv3 --kernel-trace --stats", "", "| kernel | calls | avg ms | min ms | max ms |", "|---|---|---|---|---|"]
+        hot_avg = None
         for r in csv.DictReader(open(stats)):
             lines.append(f"| {r['Name'][:70]} | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | "
                          f"{float(r['MinNs'])/1e6:.3f} | {float(r['MaxNs'])/1e6:.3f} |")
+            if HOT in r["Name"]:
+                hot_avg = float(r["AverageNs"]) / 1e6
         lines.append("")
+        if bench_line and hot_avg:
+            rf = bench_line["roofline"]
+            frac_prof = algo / (hot_avg * 1e-3) / 1e9 / rf["peak"]
+            lines += ["## Same process: bench line vs rocprof", "",
+                      f"bench (HIP events, {bench_line['steps']} timed launches): kernel {rf['kernel_ms']:.3f} ms, "
+                      f"frac {rf['frac']:.4f}; ms_per_step {bench_line['ms_per_step']:.3f}; value {bench_line['value']} GiB/s",
+                      f"rocprof average over all launches of the same process: {hot_avg:.3f} ms -> frac "
+                      f"{frac_prof:.4f} ({100 * (frac_prof / rf['frac'] - 1):+.2f} % vs the bench line)",
+                      f"build: {bench_line['config'].get('build')}", ""]
     if summary:
         lines += ["## PMC (hot kernel, mean per dispatch)", "", "| counter | value |", "|---|---|"]
         for k, v in sorted(summary.items()):

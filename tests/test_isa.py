@@ -56,8 +56,9 @@ def test_no_scalar_stores_anywhere(asm):
     """No kernel writes through the scalar data cache (gpurun refuses such code)."""
     import re
     _, text = asm
-    assert not re.search(r"^\s*(s_store_dword|s_buffer_store|s_scratch_store|s_dcache_wb|s_dcache_discard|s_atomic)",
-                         text, re.M)
+    # scalar stores (plain / buffer / scratch), scalar atomics, scalar-cache writeback or discard
+    pattern = r"^\s*s_(?:(?:buffer_|scratch_)?store|atomic|dcache_(?:wb|discard))"
+    assert not re.search(pattern, text, re.M)
 
 
 def _rotl(x, n):

@@ -268,13 +268,17 @@ def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
         rounds = 9
         r = subprocess.run([vs, "-z", "-b", "1024", "-s", "2", "-r", str(rounds), img, lst],
                            capture_output=True, text=True, timeout=300)
-        res = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {}
+        lines = r.stdout.strip().splitlines()
+        try:
+            res = json.loads(lines[-1]) if lines else {}
+        except ValueError:
+            res = {}
         out["zero_copy_verifier"] = {
             "GiB_per_s": res.get("GiB_per_s"), "digests_match": r.returncode == 0 and res.get("failed") == 0
             and res.get("ok") == res.get("chunks"), "chunks_verified": res.get("chunks"),
             "path": f"bin/verify-stream -z -b 1024 -s 2: {n} received chunks in pinned verifier slots, "
                     f"{rounds - 1} steady-state rounds timed (H2D + hash + fused memcmp + verdicts)",
-            **({} if r.returncode == 0 else {"error": r.stderr[-300:]})}
+            **({} if r.returncode == 0 else {"error": f"rc={r.returncode} {r.stderr[-300:]} {lines[-1:]}"})}
     return out
 
 

@@ -48,6 +48,11 @@ static void count(const bt_sha1_verdict *out, int m, long *good, long *bad) {
   }
 }
 
+static int cmp_resident(const void *a, const void *b) {
+  const uint8_t *x = *(const uint8_t *const *)a, *y = *(const uint8_t *const *)b;
+  return x < y ? -1 : x > y;
+}
+
 static double now(void) {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -125,6 +130,13 @@ int main(int argc, char **argv) {
     }
     per_round = ring;
   }
+  /* -z: which chunk each pinned slot holds.  The verifier hands slots out in
+   * ring order, but after a drain it resumes at whichever batch is next, so
+   * the i-th slot of a later round is not the i-th slot of round 0: every
+   * commit is paired with the chunk actually resident in the slot it got. */
+  struct resident { const uint8_t *slot; int k; } *res = NULL;
+  long nres = 0;
+  if (zcopy) res = malloc(sizeof *res * ring);
   bt_sha1_verdict out[256];
   long good = 0, bad = 0, total = 0, timed = 0;
   double t0 = now();
@@ -136,13 +148,25 @@ int main(int argc, char **argv) {
       t0 = now();
       timed = 0;
     }
+    if (zcopy && r == 1) qsort(res, nres, sizeof *res, cmp_resident);
     for (long i = 0; i < per_round; i++) {
-      const int k = (int)(i % n);
+      int k = (int)(i % n);
       const uint64_t off = (uint64_t)ids[k] * BT_CHUNK_SIZE;
       uint8_t *slot = bt_sha1_verifier_slot(v);
       if (!slot) {
         fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
         return 255;
+      }
+      if (zcopy && r == 0) {
+        res[nres].slot = slot;
+        res[nres++].k = k;
+      } else if (zcopy) {
+        struct resident key = {slot, 0}, *hit = bsearch(&key, res, nres, sizeof *res, cmp_resident);
+        if (!hit) {
+          fprintf(stderr, "verify-stream: slot %p was never filled\n", (void *)slot);
+          return 255;
+        }
+        k = hit->k;
       }
       if (!zcopy || r == 0) {
         for (uint32_t got = 0; got < BT_CHUNK_SIZE; got += PAYLOAD) { /* save_data_packet, util.c:275 */
@@ -167,6 +191,7 @@ int main(int argc, char **argv) {
   while ((m = bt_sha1_verifier_drain(v, out, 256)) > 0) count(out, m, &good, &bad);
   double dt = now() - t0;
   bt_sha1_verifier_destroy(v);
+  free(res);
   printf("{\"chunks\": %ld, \"ok\": %ld, \"failed\": %ld, \"seconds\": %.6f, \"GiB_per_s\": %.4f, \"batch\": %d, \"streams\": %d, \"poll_every\": %d, \"mode\": \"%s\"}\n",
          total, good, bad, dt, timed * (double)BT_CHUNK_SIZE / dt / (1u << 30), batch, streams, poll_every,
          zcopy ? "zero-copy slots" : "packetized memcpy (util.c:275)");

@@ -95,15 +95,28 @@ def main():
             if HOT in r["Name"]:
                 hot_avg = float(r["AverageNs"]) / 1e6
         lines.append("")
+        # The timed launches alone: the last `steps` hot-kernel dispatches of the trace.
+        trace = os.path.join(src, "prof", "bench_kernel_trace.csv")
+        timed_avg = None
+        if bench_line and os.path.exists(trace):
+            d = sorted((int(r["Dispatch_Id"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+                       for r in csv.DictReader(open(trace)) if HOT in r["Kernel_Name"])
+            last = [ms for _, ms in d[-bench_line["steps"]:]]
+            timed_avg = statistics.mean(last) if last else None
         if bench_line and hot_avg:
             rf = bench_line["roofline"]
             frac_prof = algo / (hot_avg * 1e-3) / 1e9 / rf["peak"]
+
             lines += ["## Same process: bench line vs rocprof", "",
                       f"bench (HIP events, {bench_line['steps']} timed launches): kernel {rf['kernel_ms']:.3f} ms, "
                       f"frac {rf['frac']:.4f}; ms_per_step {bench_line['ms_per_step']:.3f}; value {bench_line['value']} GiB/s",
                       f"rocprof average over all launches of the same process: {hot_avg:.3f} ms -> frac "
                       f"{frac_prof:.4f} ({100 * (frac_prof / rf['frac'] - 1):+.2f} % vs the bench line)",
                       f"build: {bench_line['config'].get('build')}", ""]
+            if timed_avg:
+                frac_timed = algo / (timed_avg * 1e-3) / 1e9 / rf["peak"]
+                lines[-1:-1] = [f"rocprof trace, the {bench_line['steps']} timed launches only: {timed_avg:.3f} ms -> "
+                                f"frac {frac_timed:.4f} ({100 * (frac_timed / rf['frac'] - 1):+.2f} % vs the bench line)"]
     if summary:
         lines += ["## PMC (hot kernel, mean per dispatch)", "", "| counter | value |", "|---|---|"]
         for k, v in sorted(summary.items()):

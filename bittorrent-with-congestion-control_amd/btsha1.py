@@ -64,6 +64,7 @@ _sig("bt_sha1_host_unregister", ctypes.c_int, _vp)
 _sig("bt_sha1_chunks_host_multi", _i64, _vp, _u64, _u64, _vp, ctypes.c_int)
 _sig("bt_sha1_chunks_host_devices", _i64, _vp, _u64, _u64, _vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int)
 _sig("bt_sha1_source_id", ctypes.c_char_p)
+_sig("bt_sha1_set_chain_batch", _u64, _u64)
 _sig("bt_sha1_kernel_name", ctypes.c_char_p, _u64)
 _sig("bt_sha1_clock_probe", ctypes.c_int, _vp, _u64, _u64, _u64, _vp, _vp, _vp)
 _sig("bt_sha1_wallclock_khz", _i64)
@@ -125,6 +126,11 @@ def set_variant(nbuf, lines=1, nt=0):
 def set_latency_batch(max_chunks):
     """Batches of <= max_chunks take the latency kernel (0: never); returns the previous value."""
     return lib.bt_sha1_set_latency_batch(max_chunks)
+
+
+def set_chain_batch(max_messages):
+    """Ragged batches of <= max_messages take the chain kernel (0: never); returns the previous setting."""
+    return lib.bt_sha1_set_chain_batch(max_messages)
 
 
 def build_info():

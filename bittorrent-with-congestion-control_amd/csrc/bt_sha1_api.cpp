@@ -130,8 +130,7 @@ struct DevCtx {
   std::mutex mu;
   hipStream_t s = nullptr;  // drop-in calls and NULL-stream launches (= lane[0].s)
   Lane lane[2];
-  DevBuf d_msg, d_state;
-  PinBuf h_msg, h_state;
+  PinBuf h_msg, h_state;  // drop-in calls: message / chaining state, read and written by the chain kernel
 };
 
 std::mutex g_ctx_mu;
@@ -547,35 +546,37 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
   return n;
 }
 
-// Single message on the GPU (shahash): stage into the aligned device buffer,
-// hash it as a one-chunk batch (the hot kernel's prefetching ring when the
-// message fits its 32-bit offsets, else the ragged kernel), 20 bytes back.
+// Single message on the GPU (shahash): copy it into the context's pinned
+// staging buffer and launch the chain kernel on it there -- the kernel reads
+// the message over PCIe itself (64 blocks per load batch, far ahead of the
+// round wave) and writes the digest straight into pinned memory -- so one
+// synchronous call is one memcpy, one launch and one stream wait: no H2D or
+// D2H copies (each a queue round trip of its own).
 int hash_one(DevCtx *c, const uint8_t *buf, uint32_t len, uint8_t out[20]) {
   if (ensure_streams(c)) return -1;
-  if (c->h_msg.ensure((size_t)len + 64) || c->d_msg.ensure((size_t)len + 64) || c->d_state.ensure(64) ||
-      c->h_state.ensure(64))
-    return -1;
+  if (c->h_msg.ensure((size_t)len + 64) || c->h_state.ensure(64)) return -1;
   if (len) memcpy(c->h_msg.p, buf, len);
-  if (len) BT_CK(hipMemcpyAsync(c->d_msg.p, c->h_msg.p, len, hipMemcpyHostToDevice, c->s));
-  if (launch_chunks(c->d_msg.p, 1, len, ((uint64_t)len + 15) & ~15ull, c->d_state.as<uint8_t>(), c->s)) return -1;
-  BT_CK(hipMemcpyAsync(c->h_state.p, c->d_state.p, 20, hipMemcpyDeviceToHost, c->s));
+  BT_CK(btsha1_launch_chain(c->h_msg.p, nullptr, nullptr, 0, len, 1, c->h_state.as<uint8_t>(), c->s));
   BT_CK(hipStreamSynchronize(c->s));
   memcpy(out, c->h_state.p, 20);
   return 0;
 }
 
-// Advance sc->hash over nblocks whole blocks at host address `blocks`.
-int midstate(DevCtx *c, uint32_t h[5], const uint8_t *blocks, uint64_t nblocks) {
-  if (!nblocks) return 0;
+// Advance h over `head` (0 or 64 bytes: SHA1Update's completed staging block)
+// followed by nblocks whole blocks at host address `blocks`: both go straight
+// into pinned memory with the state, the chain kernel reads them from there
+// and writes the state back in place (one launch, one wait per call).
+int midstate(DevCtx *c, uint32_t h[5], const uint8_t *head, const uint8_t *blocks, uint64_t nblocks) {
+  const uint64_t total = nblocks + (head ? 1 : 0);
+  if (!total) return 0;
   if (ensure_streams(c)) return -1;
-  const size_t bytes = (size_t)nblocks * 64;
-  if (c->h_msg.ensure(bytes) || c->d_msg.ensure(bytes) || c->d_state.ensure(64) || c->h_state.ensure(64)) return -1;
-  memcpy(c->h_msg.p, blocks, bytes);
+  if (c->h_msg.ensure((size_t)total * 64) || c->h_state.ensure(64)) return -1;
+  uint8_t *dst = c->h_msg.as<uint8_t>();
+  if (head) memcpy(dst, head, 64);
+  if (nblocks) memcpy(dst + (head ? 64 : 0), blocks, (size_t)nblocks * 64);
   memcpy(c->h_state.p, h, 20);
-  BT_CK(hipMemcpyAsync(c->d_msg.p, c->h_msg.p, bytes, hipMemcpyHostToDevice, c->s));
-  BT_CK(hipMemcpyAsync(c->d_state.p, c->h_state.p, 20, hipMemcpyHostToDevice, c->s));
-  BT_CK(btsha1_launch_midstate(c->d_state.as<uint32_t>(), c->d_msg.p, nblocks, c->s));
-  BT_CK(hipMemcpyAsync(c->h_state.p, c->d_state.p, 20, hipMemcpyDeviceToHost, c->s));
+  nblocks = total;
+  BT_CK(btsha1_launch_chain_midstate(c->h_state.as<uint32_t>(), c->h_msg.p, nblocks, c->s));
   BT_CK(hipStreamSynchronize(c->s));
   memcpy(h, c->h_state.p, 20);
   return 0;
@@ -636,6 +637,12 @@ int bt_sha1_set_ring_depth(int nbuf) { return bt_sha1_set_variant(nbuf, 1, 0); }
 uint64_t bt_sha1_set_latency_batch(uint64_t max_chunks) {
   const uint64_t prev = btsha1_latency_batch_setting();
   btsha1_set_latency_batch(max_chunks);
+  return prev;
+}
+
+uint64_t bt_sha1_set_chain_batch(uint64_t max_messages) {
+  const uint64_t prev = btsha1_chain_batch_setting();
+  btsha1_set_chain_batch(max_messages);
   return prev;
 }
 
@@ -982,17 +989,7 @@ void SHA1Update(SHA1Context *sc, const void *vdata, uint32_t len) {
     KeepDevice keep_dev;
     DevCtx *c = dropin_ctx("SHA1Update");
     std::lock_guard<std::mutex> g(c->mu);
-    std::vector<uint8_t> tmp;
-    const uint8_t *blocks = p;
-    uint64_t nb = nfull;
-    if (staged_full) {
-      tmp.resize(64 * (nfull + 1));
-      memcpy(tmp.data(), sc->buffer.bytes, 64);
-      if (nfull) memcpy(tmp.data() + 64, p, 64 * nfull);
-      blocks = tmp.data();
-      nb = nfull + 1;
-    }
-    if (midstate(c, sc->hash, blocks, nb)) die("SHA1Update");
+    if (midstate(c, sc->hash, staged_full ? sc->buffer.bytes : nullptr, p, nfull)) die("SHA1Update");
     sc->bufferLength = 0;
   }
   const uint32_t rest = len - (uint32_t)(64u * nfull);
@@ -1019,7 +1016,7 @@ void SHA1Final(SHA1Context *sc, uint8_t hash[SHA1_HASH_SIZE]) {
   DevCtx *c = dropin_ctx("SHA1Final");
   {
     std::lock_guard<std::mutex> g(c->mu);
-    if (midstate(c, sc->hash, blk, end / 64u)) die("SHA1Final");
+    if (midstate(c, sc->hash, nullptr, blk, end / 64u)) die("SHA1Final");
   }
   sc->totalLength += (uint64_t)(npad + 8u) * 8u;
   sc->bufferLength = 0;

@@ -504,6 +504,169 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
 }
 
 // ---------------------------------------------------------------------------
+// Chain kernel: ONE message per workgroup, for callers that wait on a single
+// serial chain (shahash, SHA1Update / SHA1Final, a handful of ragged
+// messages).  Same S / R split as k_sha1_lat, but S works across BLOCKS of
+// the one message instead of across chunks: lane j of S byte-swaps block
+// b0+j, expands its schedule and adds K (sha.c:186-200, 57-69) -- 64 blocks
+// at once -- and R runs the rounds of those 64 blocks back to back from LDS
+// (broadcast ds_read_b128, 5 VALU per round).  One barrier per 64 blocks
+// instead of one per block, and S is never on R's critical path (it finishes
+// a batch in a few microseconds; R takes ~50).  S reads the message wherever
+// it is -- device memory, or pinned host memory directly over PCIe, so the
+// drop-in calls need no H2D copy -- and builds the MD padding block(s)
+// itself (sha.c:529-543).
+//   MID = true : SHA1Update/SHA1Final midstate -- state[5] (SHA1Context.hash
+//                order) advanced over fixed_len/64 whole blocks of `base`.
+//   MID = false: message i = base + (offsets ? offsets[i] : i*pitch), length
+//                lens ? lens[i] : fixed_len, digest i (big-endian, any
+//                alignment) to digests + 20*i.  blockIdx.x = message.
+// Barrier accounting as in k_sha1_lat: both waves execute nbatch + 1.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kChainBatch = 64;  // blocks per LDS slot = lanes of S
+
+// Block g of a message (nfull whole blocks, r tail bytes, bits total length)
+// as 16 big-endian words: message block, tail block or length-only block.
+template <bool MID>
+__device__ __forceinline__ void chain_block(uint32_t (&w)[16], const uint8_t *p, uint64_t g, uint64_t nfull, uint32_t r,
+                                            uint64_t bits) {
+  if (g < nfull) {
+    u32x4 q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) __builtin_memcpy(&q[i], p + 64 * g + 16 * i, 16);  // any alignment
+    block_from_le(w, q[0], q[1], q[2], q[3]);
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) w[j] = 0u;
+  if constexpr (!MID) {
+    if (g == nfull) {  // tail bytes + 0x80 (+ the length when r <= 55)
+      const uint8_t *t = p + 64 * nfull;
+      for (uint32_t k = 0; k < r; ++k) w[k >> 2] |= (uint32_t)t[k] << (24 - 8 * (k & 3));
+      w[r >> 2] |= 0x80000000u >> ((r & 3) * 8);
+      if (r < 56) {
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+      }
+    } else {  // r >= 56: a length-only block follows
+      w[14] = (uint32_t)(bits >> 32);
+      w[15] = (uint32_t)bits;
+    }
+  }
+}
+
+// R side of the chain kernel: one block's W+K words from an LDS slot
+// (broadcast: every lane reads the same 16 bytes) and the 80 rounds on them.
+__device__ __forceinline__ void chain_fetch(u32x4 (&q)[20], const u32x4 *slot, uint32_t k) {
+#pragma unroll
+  for (int j = 0; j < 20; ++j) q[j] = slot[j * kChainBatch + k];
+}
+
+template <int T>
+__device__ __forceinline__ void rounds_wk_regs(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
+                                               const u32x4 (&q)[20]) {
+  if constexpr (T < 80) {
+    const u32x4 v = q[T / 4];
+    round_wk<T>(a, b, c, d, e, v.x);
+    round_wk<T + 1>(a, b, c, d, e, v.y);
+    round_wk<T + 2>(a, b, c, d, e, v.z);
+    round_wk<T + 3>(a, b, c, d, e, v.w);
+    rounds_wk_regs<T + 4>(a, b, c, d, e, q);
+  }
+}
+
+__device__ __forceinline__ void chain_rounds(State &st, const u32x4 (&q)[20]) {
+  uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
+  rounds_wk_regs<0>(a, b, c, d, e, q);
+  st.h0 += a;  // sha.c:446-450
+  st.h1 += b;
+  st.h2 += c;
+  st.h3 += d;
+  st.h4 += e;
+}
+
+template <bool MID>
+__global__ __launch_bounds__(128) void k_sha1_chain(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offsets,
+                                                    const uint32_t *__restrict__ lens, uint64_t pitch, uint64_t fixed_len,
+                                                    uint32_t *__restrict__ state, uint8_t *__restrict__ digests) {
+  __shared__ u32x4 lds[2][20 * kChainBatch];  // 2 slots x 64 blocks x 80 W+K words = 40 KiB
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t i = blockIdx.x;
+  const uint8_t *p = base + (offsets ? offsets[i] : i * pitch);
+  const uint64_t len = lens ? (uint64_t)lens[i] : fixed_len;
+  const uint64_t nfull = len >> 6;
+  const uint32_t r = (uint32_t)(len & 63u);
+  const uint64_t nb_total = MID ? nfull : nfull + (r >= 56u ? 2u : 1u);
+  const uint64_t nbatch = (nb_total + kChainBatch - 1) / kChainBatch;
+  uint32_t nbar = 0;
+  (void)nbar;
+  if (wave == 0) {
+    // ---- S: lane j prepares block b0 + j ----------------------------------
+    for (uint64_t bt = 0; bt < nbatch; ++bt) {
+      const uint64_t g = bt * kChainBatch + lane;
+      uint32_t w[16];
+      chain_block<MID>(w, p, g < nb_total ? g : nb_total, nfull, r, len * 8ull);
+      produce_wk<0, 80>(w, lds[bt & 1u], lane);
+      BT_LAT_BARRIER(nbar);
+    }
+    BT_LAT_BARRIER(nbar);  // pairs with R's last barrier
+    BT_LAT_CHECK(nbar, nbatch + 1u);
+  } else {
+    // ---- R: the chain --------------------------------------------------------
+    State st;
+    if constexpr (MID) {
+      st.h0 = state[0]; st.h1 = state[1]; st.h2 = state[2]; st.h3 = state[3]; st.h4 = state[4];
+    } else {
+      st.init();
+    }
+    // R's 64 lanes run the same chain off broadcast LDS reads, so every value
+    // is uniform; left alone, hipcc proves that, keeps the chaining state in
+    // SGPRs and pays v_readfirstlane + split adds per block (488 VALU instead
+    // of 405, seen in the ISA).  An opaque zero in a VGPR keeps the chain in
+    // VGPRs, where the round is 5 VALU (bitop3, 2 alignbit, add3, add).
+    uint32_t vzero;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+    BT_LAT_BARRIER(nbar);  // batch 0 is in slot 0
+    for (uint64_t bt = 0; bt < nbatch; ++bt) {
+      const u32x4 *slot = lds[bt & 1u] + vzero;
+      const uint64_t left = nb_total - bt * kChainBatch;
+      const uint32_t nb = left < kChainBatch ? (uint32_t)left : kChainBatch;
+      // Two register buffers of a block's 80 W+K words: block k+1 is read
+      // (broadcast ds_read_b128) while block k's rounds run, so the rounds
+      // never wait on LDS and the loop carries one lgkmcnt wait per block.
+      u32x4 wa[20], wb[20];
+      chain_fetch(wa, slot, 0);
+      uint32_t k = 0;
+      for (; k + 2 <= nb; k += 2) {
+        chain_fetch(wb, slot, k + 1);
+        chain_rounds(st, wa);
+        chain_fetch(wa, slot, k + 2 < nb ? k + 2 : nb - 1);
+        chain_rounds(st, wb);
+      }
+      if (k < nb) chain_rounds(st, wa);
+      BT_LAT_BARRIER(nbar);
+    }
+    BT_LAT_CHECK(nbar, nbatch + 1u);
+    if (lane == 0) {
+      if constexpr (MID) {
+        state[0] = st.h0; state[1] = st.h1; state[2] = st.h2; state[3] = st.h3; state[4] = st.h4;
+      } else {
+        uint8_t *o = digests + 20 * i;
+        const uint32_t h[5] = {st.h0, st.h1, st.h2, st.h3, st.h4};
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {  // sha.c:550-553
+          o[4 * k] = (uint8_t)(h[k] >> 24);
+          o[4 * k + 1] = (uint8_t)(h[k] >> 16);
+          o[4 * k + 2] = (uint8_t)(h[k] >> 8);
+          o[4 * k + 3] = (uint8_t)h[k];
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generic paths (64-bit addressing, any alignment).
 // ---------------------------------------------------------------------------
 // Block source for absorb_ring: how one 64-byte block is fetched into a
@@ -841,9 +1004,22 @@ const char *btsha1_fixed_kernel_name(uint64_t n, int variant) {
   return "k_sha1_fixed";
 }
 
+// Ragged batches of at most this many messages take the chain kernel (one
+// two-wave workgroup per message; 0: never).  Default: one per CU.
+static uint64_t g_chain_max = BT_SHA1_CHAIN_AUTO;
+void btsha1_set_chain_batch(uint64_t max_messages) { __atomic_store_n(&g_chain_max, max_messages, __ATOMIC_RELAXED); }
+uint64_t btsha1_chain_batch_setting() { return __atomic_load_n(&g_chain_max, __ATOMIC_RELAXED); }
+uint64_t btsha1_chain_batch() {
+  const uint64_t v = btsha1_chain_batch_setting();
+  return v == BT_SHA1_CHAIN_AUTO ? (uint64_t)btsha1_device_cus() : v;
+}
+
 hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t pitch,
                                 uint32_t fixed_len, uint64_t n, uint8_t *d_dig, hipStream_t s) {
   if (n == 0) return hipSuccess;
+  // A few messages: each one's latency is its serial chain, which the chain
+  // kernel runs at ~405 VALU per block instead of the ragged kernel's ~600.
+  if (n <= btsha1_chain_batch()) return btsha1_launch_chain(d_base, d_off, d_len, pitch, fixed_len, n, d_dig, s);
   // As launch_fixed_v: below one wave per SIMD, one-wave workgroups spread
   // the chains over CUs (each message is a serial chain).
   const uint32_t wg = chain_workgroup(n);
@@ -855,6 +1031,22 @@ hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const
 
 hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_t nblocks, hipStream_t s) {
   hipLaunchKernelGGL(k_sha1_midstate, dim3(1), dim3(64), 0, s, d_state, (const uint8_t *)d_data, nblocks);
+  return hipGetLastError();
+}
+
+hipError_t btsha1_launch_chain_midstate(uint32_t *state, const void *data, uint64_t nblocks, hipStream_t s) {
+  if (nblocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sha1_chain<true>, dim3(1), dim3(128), 0, s, (const uint8_t *)data, nullptr, nullptr, 0ull,
+                     nblocks * 64ull, state, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t btsha1_launch_chain(const void *base, const uint64_t *offsets, const uint32_t *lens, uint64_t pitch,
+                               uint64_t fixed_len, uint64_t n, uint8_t *digests, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (n > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_sha1_chain<false>, dim3((uint32_t)n), dim3(128), 0, s, (const uint8_t *)base, offsets, lens, pitch,
+                     fixed_len, nullptr, digests);
   return hipGetLastError();
 }
 

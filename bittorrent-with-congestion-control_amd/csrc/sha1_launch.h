@@ -29,16 +29,29 @@ const char *btsha1_fixed_kernel_name(uint64_t n, int variant);
 void btsha1_set_latency_batch(uint64_t max_chunks);
 uint64_t btsha1_latency_batch_setting();  // raw setting (may be BT_SHA1_LATENCY_AUTO)
 uint64_t btsha1_latency_batch();          // effective threshold on the current device
+#define BT_SHA1_CHAIN_AUTO UINT64_MAX  // = CUs of the launching device
+void btsha1_set_chain_batch(uint64_t max_messages);
+uint64_t btsha1_chain_batch_setting();
+uint64_t btsha1_chain_batch();
 // Compute units of the current device (cached per device; 256 on MI355X).
 uint32_t btsha1_device_cus();
 // Hot-kernel variant code = ring slots*100 + lines per slot*10 + nt flag.
 bool btsha1_fixed_variant_ok(int code);
 // n messages at d_base + d_off[i], d_len[i] bytes each; with d_off == NULL,
-// message i is at d_base + i*pitch, fixed_len bytes.  Any alignment.
+// message i is at d_base + i*pitch, fixed_len bytes.  Any alignment.  At most
+// btsha1_chain_batch() messages take the chain kernel, more the one-message-
+// per-lane ragged kernel.
 hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t pitch,
                                 uint32_t fixed_len, uint64_t n, uint8_t *d_dig, hipStream_t s);
 // d_state[5] advanced over nblocks whole 64-byte blocks at d_data.
 hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_t nblocks, hipStream_t s);
+// Chain kernel (one message per two-wave workgroup; lowest single-chain
+// latency).  state / data may be device or pinned host memory.
+hipError_t btsha1_launch_chain_midstate(uint32_t *state, const void *data, uint64_t nblocks, hipStream_t s);
+// n messages: message i at base + (offsets ? offsets[i] : i*pitch), length
+// lens ? lens[i] : fixed_len; digest i (big-endian bytes) at digests + 20*i.
+hipError_t btsha1_launch_chain(const void *base, const uint64_t *offsets, const uint32_t *lens, uint64_t pitch,
+                               uint64_t fixed_len, uint64_t n, uint8_t *digests, hipStream_t s);
 // Synthetic stream words [first_word, first_word + nbytes/8) into d_buf (16-byte aligned).
 hipError_t btsha1_launch_fill(void *d_buf, uint64_t nbytes, uint64_t first_word, uint64_t seed, hipStream_t s);
 // Digest lookup: d_index[q] = smallest i with table[i] == queries[q], else -1.

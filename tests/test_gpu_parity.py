@@ -55,9 +55,10 @@ def test_shahash_kats(bt):
 
 
 def test_shahash_either_side_of_the_hot_kernel_limit(bt, oracle):
-    """shahash takes the hot kernel while 64*pitch + 4096 fits 32-bit buffer
-    offsets (messages up to ~64 MiB) and the ragged kernel past it; both
-    sides of the limit, plus short messages at every residue mod 64."""
+    """shahash runs the chain kernel on the pinned staging copy: messages on
+    both sides of the hot kernel's 32-bit offset limit (~64 MiB, where the
+    fixed-layout paths switch kernels), plus short messages at every residue
+    mod 64 (one or two padding blocks built by the loader wave)."""
     limit = ((1 << 32) - 4096) // 64  # largest 16-byte pitch the hot kernel takes
     for n in (limit - 16 - 7, limit + 1):
         msg = bytes(oracle.fill_synthetic(n, n, 0x51A7))
@@ -88,7 +89,24 @@ def test_streaming_context_fields(bt, oracle):
         [0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476, 0xc3d2e1f0], b"x" * 64)
 
 
-def test_edge_lengths_ragged_kernel(bt, torch, oracle):
+@contextlib.contextmanager
+def ragged_mode(bt, mode):
+    """Pin ragged batches to the chain kernel ("chain": one workgroup per
+    message) or to the one-message-per-lane ragged kernel ("lanes")."""
+    prev = bt.set_chain_batch(1 << 62 if mode == "chain" else 0)
+    try:
+        yield
+    finally:
+        bt.set_chain_batch(prev)
+
+
+@pytest.fixture(params=["chain", "lanes"])
+def rmode(bt, request):
+    with ragged_mode(bt, request.param):
+        yield request.param
+
+
+def test_edge_lengths_ragged_kernel(bt, torch, oracle, rmode):
     rows = read_pairs("edge_lengths.txt")
     stream = bytes(oracle.fill_synthetic(max(int(n) for n, _ in rows), 0, oracle.SEED_EDGE))
     d = to_dev(torch, stream)
@@ -101,7 +119,7 @@ def test_edge_lengths_ragged_kernel(bt, torch, oracle):
     assert [x.hex() for x in digests_of(torch, out, n)] == [h for _, h in rows]
 
 
-def test_ragged_golden_batch_unaligned(bt, torch, oracle):
+def test_ragged_golden_batch_unaligned(bt, torch, oracle, rmode):
     rows = read_pairs("ragged.txt")
     msgs = [bytes(oracle.fill_synthetic(int(n), int(k) * 1024, oracle.SEED_RAGGED)) for k, n, _ in rows]
     # pack with deliberately odd offsets (1..7 bytes of slack) to hit every alignment
@@ -656,7 +674,7 @@ def test_peer_download_flow_end_to_end(bt, torch, tmp_path):
     assert out.read_bytes() == img  # diff A.tar test1.tar
 
 
-def test_randomized_layouts_vs_oracle(bt, torch, oracle):
+def test_randomized_layouts_vs_oracle(bt, torch, oracle, rmode):
     """Seeded random batches: chunk length, pitch, count, input offset (alignment)
     and digest-output offset drawn at random, so both the hot kernel (aligned
     layouts) and the generic kernel (anything else) see shapes no fixed case
@@ -781,3 +799,50 @@ def test_clock_probe_stamps_and_digests(bt, torch, oracle):
     assert bool((dm > 0).all()) and bool((dr > 0).all())
     mhz = float((dm / dr).median()) * bt.wallclock_khz() / 1000.0
     assert 500.0 < mhz < 3000.0, mhz
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 129, 200])
+def test_chain_kernel_many_blocks_and_batches(bt, torch, oracle, n):
+    """Chain kernel batch boundaries: messages whose block counts straddle the
+    loader wave's 64-block batches (and the two LDS slots), with every
+    padding residue, against the oracle."""
+    with ragged_mode(bt, "chain"):
+        lens = [64 * n + r for r in (0, 1, 55, 56, 63)] + [64 * n - 8, 64 * 64 * 2 + n]
+        blob = bytes(oracle.fill_synthetic(sum(lens) + 64, n, 0xC4A1))
+        offs, o = [], 0
+        for L in lens:
+            offs.append(o)
+            o += L
+        d = to_dev(torch, blob)
+        ot = torch.tensor(offs, dtype=torch.int64, device="cuda")
+        lt = torch.tensor(lens, dtype=torch.int32, device="cuda")
+        out = torch.zeros(20 * len(lens) + 3, dtype=torch.uint8, device="cuda")
+        bt.ragged_dev(d.data_ptr(), ot.data_ptr(), lt.data_ptr(), len(lens), out.data_ptr() + 3)
+        torch.cuda.synchronize()
+        raw = bytes(out.cpu().numpy().tobytes())[3:]
+        for i, (off, L) in enumerate(zip(offs, lens)):
+            assert raw[20 * i:20 * i + 20] == oracle.sha1(blob[off:off + L]), (n, L)
+
+
+def test_streaming_update_pieces_and_context(bt, oracle):
+    """SHA1Update through the chain kernel's midstate mode, fed the way the
+    peer receives a chunk (1484-byte DATA payloads, util.c:275) and in odd
+    pieces, with SHA1Context.hash / totalLength / bufferLength checked after
+    every call against the oracle's own streaming context."""
+    msg = bytes(oracle.fill_synthetic(CHUNK, 0, oracle.SEED_SYNTH))
+    s = bt.Sha1()
+    o = oracle.Sha1Stream()
+    i, k = 0, 0
+    pieces = [1484, 1, 63, 64, 65, 4096, 1484 * 7, 100000]
+    while i < len(msg):
+        j = min(len(msg), i + pieces[k % len(pieces)])
+        s.update(msg[i:j])
+        o.update(msg[i:j])
+        k += 1
+        i = j
+        assert s.ctx.totalLength == 8 * i and s.ctx.bufferLength == i % 64
+        if k % 17 == 0:
+            done = i - i % 64
+            assert list(s.ctx.hash) == oracle.compress_blocks(
+                [0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476, 0xc3d2e1f0], msg[:done]), k
+    assert s.final() == o.final() == oracle.sha1(msg)

@@ -66,7 +66,7 @@ def main():
     assert got == want
     emit("shahash_512k", ts)
 
-    s = torch.cuda.Stream()  # a real stream: handle 0 would mean "library stream" to the C-ABI
+    s = torch.cuda.Stream()
     torch.cuda.set_stream(s)
     dev = torch.empty(CHUNK + 4096, dtype=torch.uint8, device="cuda")
     out = torch.zeros(20 * 4096, dtype=torch.uint8, device="cuda")
@@ -84,11 +84,15 @@ def main():
             res.append(a.elapsed_time(b) * 1e-3)
         return res[1:]
 
-    for name, off in (("ragged_1x512k", 0), ("ragged_1x512k_u", 3)):
-        dev[off:off + CHUNK].copy_(torch.frombuffer(bytearray(msg), dtype=torch.uint8))
-        ts = ragged(dev.data_ptr(), [off], [CHUNK])
-        assert bytes(out[:20].cpu().numpy().tobytes()) == want, name
-        emit(name, ts, {"kernel": "k_sha1_ragged"})
+    prev_chain = bt.set_chain_batch(0)
+    for kname, thr in (("k_sha1_ragged", 0), ("k_sha1_chain", 1 << 62)):
+        bt.set_chain_batch(thr)
+        for name, off in (("ragged_1x512k", 0), ("ragged_1x512k_u", 3)):
+            dev[off:off + CHUNK].copy_(torch.frombuffer(bytearray(msg), dtype=torch.uint8))
+            ts = ragged(dev.data_ptr(), [off], [CHUNK])
+            assert bytes(out[:20].cpu().numpy().tobytes()) == want, name
+            emit(name + ("_chain" if thr else ""), ts, {"kernel": kname})
+    bt.set_chain_batch(0)
 
     n = 4096
     lens = [int(x) for x in rng.integers(480 * 1024, 544 * 1024, n)]
@@ -154,6 +158,25 @@ def main():
             med = statistics.median(res[1:])
             emit(f"batch_{n}_{mode}", res[1:], {"chunks": n, "GiB_per_s": round(n * CHUNK / med / 2**30, 2)})
     bt.set_latency_batch(prev)
+    # The same chunks as ragged messages through the chain kernel (one
+    # two-wave workgroup per chunk).
+    bt.set_chain_batch(1 << 62)
+    for n in (1, 64, 256):
+        o = torch.arange(n, dtype=torch.int64, device="cuda") * CHUNK
+        ln = torch.full((n,), CHUNK, dtype=torch.int32, device="cuda")
+        res = []
+        for _ in range(max(3, args.reps // 2) + 1):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            bt.ragged_dev(big.data_ptr(), o.data_ptr(), ln.data_ptr(), n, dig.data_ptr(), s.cuda_stream)
+            b.record(s)
+            torch.cuda.synchronize()
+            res.append(a.elapsed_time(b) * 1e-3)
+        raw = dig[:20 * n].cpu().numpy().tobytes()
+        assert all(raw[20 * i:20 * i + 20].hex() == golden[i] for i in range(n)), ("chain", n)
+        med = statistics.median(res[1:])
+        emit(f"batch_{n}_chain", res[1:], {"chunks": n, "GiB_per_s": round(n * CHUNK / med / 2**30, 2)})
+    bt.set_chain_batch(prev_chain)
     del big
 
     v = bt.Verifier(batch=1, nstreams=2)

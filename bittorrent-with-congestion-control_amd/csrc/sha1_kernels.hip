@@ -585,16 +585,19 @@ __device__ __forceinline__ void chain_rounds(State &st, const u32x4 (&q)[20]) {
   st.h4 += e;
 }
 
-template <bool MID>
+template <bool MID, bool VERIFY = false>
 __global__ __launch_bounds__(128) void k_sha1_chain(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offsets,
                                                     const uint32_t *__restrict__ lens, uint64_t pitch, uint64_t fixed_len,
-                                                    uint32_t *__restrict__ state, uint8_t *__restrict__ digests) {
+                                                    uint64_t tail_len, uint32_t *__restrict__ state,
+                                                    uint8_t *__restrict__ digests, const uint8_t *__restrict__ expected,
+                                                    uint8_t *__restrict__ ok) {
   __shared__ u32x4 lds[2][20 * kChainBatch];  // 2 slots x 64 blocks x 80 W+K words = 40 KiB
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t i = blockIdx.x;
   const uint8_t *p = base + (offsets ? offsets[i] : i * pitch);
-  const uint64_t len = lens ? (uint64_t)lens[i] : fixed_len;
+  // tail_len != 0: the last message is a shorter one (make_chunks' last fread).
+  const uint64_t len = lens ? (uint64_t)lens[i] : (tail_len && i + 1 == gridDim.x ? tail_len : fixed_len);
   const uint64_t nfull = len >> 6;
   const uint32_t r = (uint32_t)(len & 63u);
   const uint64_t nb_total = MID ? nfull : nfull + (r >= 56u ? 2u : 1u);
@@ -652,14 +655,23 @@ __global__ __launch_bounds__(128) void k_sha1_chain(const uint8_t *__restrict__ 
       if constexpr (MID) {
         state[0] = st.h0; state[1] = st.h1; state[2] = st.h2; state[3] = st.h3; state[4] = st.h4;
       } else {
-        uint8_t *o = digests + 20 * i;
         const uint32_t h[5] = {st.h0, st.h1, st.h2, st.h3, st.h4};
+        if (digests) {
+          uint8_t *o = digests + 20 * i;
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {  // sha.c:550-553
-          o[4 * k] = (uint8_t)(h[k] >> 24);
-          o[4 * k + 1] = (uint8_t)(h[k] >> 16);
-          o[4 * k + 2] = (uint8_t)(h[k] >> 8);
-          o[4 * k + 3] = (uint8_t)h[k];
+          for (int k = 0; k < 5; ++k) {  // sha.c:550-553
+            o[4 * k] = (uint8_t)(h[k] >> 24);
+            o[4 * k + 1] = (uint8_t)(h[k] >> 16);
+            o[4 * k + 2] = (uint8_t)(h[k] >> 8);
+            o[4 * k + 3] = (uint8_t)h[k];
+          }
+        }
+        if constexpr (VERIFY) {  // memcmp(hash, chunk->hash, 20) == 0, util.c:313
+          const uint8_t *x = expected + 20 * i;
+          uint32_t diff = 0;
+#pragma unroll
+          for (int k = 0; k < 20; ++k) diff |= (uint32_t)x[k] ^ ((h[k >> 2] >> (24 - 8 * (k & 3))) & 0xFFu);
+          ok[i] = diff == 0;
         }
       }
     }
@@ -965,7 +977,12 @@ hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uin
                                const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, int variant, uint32_t tail_len) {
   if (tail_len && d_ok) return hipErrorInvalidValue;  // verify batches are whole chunks
   if (n == 0 && tail_len == 0) return hipSuccess;
-  if (n + (tail_len ? 1 : 0) <= btsha1_latency_batch()) return launch_lat(d_in, n, pitch, len, d_dig, d_exp, d_ok, s, tail_len);
+  const uint64_t total = n + (tail_len ? 1 : 0);
+  // Up to one chunk per CU: a two-wave workgroup per chunk (chain kernel);
+  // up to 64 per CU: 64 chunks per two-wave workgroup (latency kernel).
+  if (total <= btsha1_chain_batch() && total <= btsha1_latency_batch())
+    return btsha1_launch_chain(d_in, nullptr, nullptr, pitch, len, n, d_dig, s, tail_len, d_exp, d_ok);
+  if (total <= btsha1_latency_batch()) return launch_lat(d_in, n, pitch, len, d_dig, d_exp, d_ok, s, tail_len);
   if (variant == kLdsVariant || variant == kLdsNtVariant) {
     if (n) {
       const hipError_t e = variant == kLdsVariant ? launch_lds<0>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s)
@@ -999,6 +1016,7 @@ hipError_t btsha1_launch_fixed_stamped(const void *d_in, uint64_t n, uint32_t pi
 
 const char *btsha1_fixed_kernel_name(uint64_t n, int variant) {
   if (n == 0) return "none";
+  if (n <= btsha1_chain_batch() && n <= btsha1_latency_batch()) return "k_sha1_chain";
   if (n <= btsha1_latency_batch()) return "k_sha1_lat";
   if (variant == kLdsVariant || variant == kLdsNtVariant) return "k_sha1_lds";
   return "k_sha1_fixed";
@@ -1019,7 +1037,7 @@ hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const
   if (n == 0) return hipSuccess;
   // A few messages: each one's latency is its serial chain, which the chain
   // kernel runs at ~405 VALU per block instead of the ragged kernel's ~600.
-  if (n <= btsha1_chain_batch()) return btsha1_launch_chain(d_base, d_off, d_len, pitch, fixed_len, n, d_dig, s);
+  if (n <= btsha1_chain_batch()) return btsha1_launch_chain(d_base, d_off, d_len, pitch, fixed_len, n, d_dig, s, 0, nullptr, nullptr);
   // As launch_fixed_v: below one wave per SIMD, one-wave workgroups spread
   // the chains over CUs (each message is a serial chain).
   const uint32_t wg = chain_workgroup(n);
@@ -1037,16 +1055,22 @@ hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_
 hipError_t btsha1_launch_chain_midstate(uint32_t *state, const void *data, uint64_t nblocks, hipStream_t s) {
   if (nblocks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sha1_chain<true>, dim3(1), dim3(128), 0, s, (const uint8_t *)data, nullptr, nullptr, 0ull,
-                     nblocks * 64ull, state, nullptr);
+                     nblocks * 64ull, 0ull, state, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 
 hipError_t btsha1_launch_chain(const void *base, const uint64_t *offsets, const uint32_t *lens, uint64_t pitch,
-                               uint64_t fixed_len, uint64_t n, uint8_t *digests, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  if (n > 0x7fffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_sha1_chain<false>, dim3((uint32_t)n), dim3(128), 0, s, (const uint8_t *)base, offsets, lens, pitch,
-                     fixed_len, nullptr, digests);
+                               uint64_t fixed_len, uint64_t n, uint8_t *digests, hipStream_t s, uint64_t tail_len,
+                               const uint8_t *expected, uint8_t *ok) {
+  const uint64_t grid = n + (tail_len ? 1 : 0);
+  if (grid == 0) return hipSuccess;
+  if (grid > 0x7fffffffull || (ok && (offsets || tail_len))) return hipErrorInvalidValue;
+  if (ok)
+    hipLaunchKernelGGL((k_sha1_chain<false, true>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)base, offsets,
+                       lens, pitch, fixed_len, tail_len, nullptr, digests, expected, ok);
+  else
+    hipLaunchKernelGGL((k_sha1_chain<false, false>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)base,
+                       offsets, lens, pitch, fixed_len, tail_len, nullptr, digests, expected, ok);
   return hipGetLastError();
 }
 

@@ -49,9 +49,13 @@ hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_
 // latency).  state / data may be device or pinned host memory.
 hipError_t btsha1_launch_chain_midstate(uint32_t *state, const void *data, uint64_t nblocks, hipStream_t s);
 // n messages: message i at base + (offsets ? offsets[i] : i*pitch), length
-// lens ? lens[i] : fixed_len; digest i (big-endian bytes) at digests + 20*i.
+// lens ? lens[i] : fixed_len; digest i (big-endian bytes) at digests + 20*i
+// (digests may be NULL with ok).  tail_len != 0 (no offsets): one more message
+// of tail_len bytes at base + n*pitch.  ok != NULL (no offsets, no tail):
+// ok[i] = digest i == expected[20*i ..] (util.c:313).
 hipError_t btsha1_launch_chain(const void *base, const uint64_t *offsets, const uint32_t *lens, uint64_t pitch,
-                               uint64_t fixed_len, uint64_t n, uint8_t *digests, hipStream_t s);
+                               uint64_t fixed_len, uint64_t n, uint8_t *digests, hipStream_t s, uint64_t tail_len = 0,
+                               const uint8_t *expected = nullptr, uint8_t *ok = nullptr);
 // Synthetic stream words [first_word, first_word + nbytes/8) into d_buf (16-byte aligned).
 hipError_t btsha1_launch_fill(void *d_buf, uint64_t nbytes, uint64_t first_word, uint64_t seed, hipStream_t s);
 // Digest lookup: d_index[q] = smallest i with table[i] == queries[q], else -1.

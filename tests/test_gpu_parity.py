@@ -157,24 +157,28 @@ def synth4096(bt, torch, oracle):
 
 LDS = 10  # bt_sha1_set_ring_depth(10): the LDS-staged hot kernel (k_sha1_lds)
 LAT = "lat"  # bt_sha1_set_latency_batch: the two-wave latency kernel (k_sha1_lat)
+CHAIN = "chain"  # bt_sha1_set_chain_batch: one two-wave workgroup per chunk (k_sha1_chain)
 
 
 @contextlib.contextmanager
 def kernel_mode(bt, mode):
-    """Pin the fixed-layout launches to one kernel: LAT, a ring depth or a
-    (nbuf, lines, nt) variant (latency kernel off).  Restores the defaults."""
-    prev = bt.set_latency_batch(1 << 62 if mode == LAT else 0)
-    if mode != LAT:
+    """Pin the fixed-layout launches to one kernel: LAT, CHAIN, a ring depth or
+    a (nbuf, lines, nt) variant (latency and chain kernels off).  Restores the
+    defaults."""
+    prev = bt.set_latency_batch(1 << 62 if mode in (LAT, CHAIN) else 0)
+    prev_chain = bt.set_chain_batch(1 << 62 if mode == CHAIN else 0)
+    if mode not in (LAT, CHAIN):
         bt.set_variant(*(mode if isinstance(mode, tuple) else (mode, 1, 0)))
     try:
         yield
     finally:
         bt.set_variant(3, 1, 0)
         bt.set_latency_batch(prev)
+        bt.set_chain_batch(prev_chain)
 
 
 @pytest.mark.parametrize("variant", [(2, 1, 0), (3, 1, 0), (4, 1, 0), (2, 2, 0), (3, 1, 1), (LDS, 1, 0), (LDS, 1, 1),
-                                     LAT])
+                                     LAT, CHAIN])
 def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, variant):
     """BASELINE config 2: 4096 synthetic 512 KiB chunks, every digest == sha.c's,
     for every compiled hot-kernel variant (ring depth, slot lines, nt, LDS-staged)
@@ -189,7 +193,7 @@ def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, variant):
         assert got == read_pairs("synth4096.txt")
 
 
-@pytest.mark.parametrize("ring", [3, LDS, LAT])
+@pytest.mark.parametrize("ring", [3, LDS, LAT, CHAIN])
 def test_verify_dev_flags_mismatches(bt, torch, synth4096, ring):
     with kernel_mode(bt, ring):
         _verify_dev_flags_mismatches(bt, torch, synth4096)
@@ -220,7 +224,7 @@ def _verify_dev_flags_mismatches(bt, torch, synth4096):
     (1000, 1003, 67),            # odd pitch -> generic kernel
     (CHUNK, CHUNK + 256, 65),    # padded pitch, fast kernel
 ])
-@pytest.mark.parametrize("ring", [3, LDS, LAT])
+@pytest.mark.parametrize("ring", [3, LDS, LAT, CHAIN])
 def test_fixed_layouts_vs_oracle(bt, torch, oracle, chunk_len, pitch, n, ring):
     total = pitch * (n - 1) + chunk_len
     host = bytearray(oracle.fill_synthetic(total, 11, 0xC0FFEE))
@@ -234,7 +238,7 @@ def test_fixed_layouts_vs_oracle(bt, torch, oracle, chunk_len, pitch, n, ring):
 
 
 def _ragged_line_counts(bt, torch, oracle, ring):
-    deepest = 4 if ring in (LDS, LAT) else ring
+    deepest = 4 if ring in (LDS, LAT, CHAIN) else ring
     for blocks in range(0, 2 * 2 * deepest + 3):
         for r in (0, 5, 56):
             L = 64 * blocks + r
@@ -251,7 +255,7 @@ def _ragged_line_counts(bt, torch, oracle, ring):
 
 
 def test_every_ring_depth_on_ragged_line_counts(bt, torch, oracle):
-    for ring in (2, 3, 4, LDS, LAT):
+    for ring in (2, 3, 4, LDS, LAT, CHAIN):
         with kernel_mode(bt, ring):
             _ragged_line_counts(bt, torch, oracle, ring)
 
@@ -271,7 +275,7 @@ def test_host_pipeline_c_tar_and_tail(bt, oracle):
     assert bt.chunks_host(big, chunk_len=4096) == oracle.hash_chunks(big, 4096)
 
 
-@pytest.mark.parametrize("variant", [(3, 1, 0), (2, 2, 0), (LDS, 1, 0), LAT])
+@pytest.mark.parametrize("variant", [(3, 1, 0), (2, 2, 0), (LDS, 1, 0), LAT, CHAIN])
 def test_image_tail_in_same_launch(bt, oracle, variant):
     """launch_image: the short last chunk rides in the hot kernel's (or the
     latency kernel's) tail wave; the LDS-staged variant hands it to the ragged
@@ -772,13 +776,17 @@ def test_null_stream_orders_after_default_stream_work(bt, torch, oracle):
 
 def test_kernel_name_reports_the_launch(bt):
     lat = bt.set_latency_batch(2**64 - 1)  # auto
+    chain = bt.set_chain_batch(2**64 - 1)
     try:
-        assert bt.kernel_name(1) == "k_sha1_lat"
-        assert bt.kernel_name(16384) == "k_sha1_lat"  # 64 per CU on a 256-CU MI355X
+        assert bt.kernel_name(1) == "k_sha1_chain"
+        assert bt.kernel_name(256) == "k_sha1_chain"  # one per CU on a 256-CU MI355X
+        assert bt.kernel_name(257) == "k_sha1_lat"
+        assert bt.kernel_name(16384) == "k_sha1_lat"  # 64 per CU
         assert bt.kernel_name(131072) == "k_sha1_fixed"
         assert "latency_batch=auto" in bt.build_info()
     finally:
         bt.set_latency_batch(lat)
+        bt.set_chain_batch(chain)
 
 
 def test_clock_probe_stamps_and_digests(bt, torch, oracle):

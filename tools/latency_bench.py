@@ -142,9 +142,13 @@ def main():
             i, h = line.split()
             golden[int(i)] = h
     prev = bt.set_latency_batch(0)
-    for n in (1, 64, 1024, 4096, 16384, 32768, 65536):
-        for mode, thr in (("fixed", 0), ("lat", 1 << 62)):
+    prev_chain_fixed = bt.set_chain_batch(0)
+    for n in (1, 64, 256, 1024, 4096, 16384, 32768, 65536):
+        for mode, thr, cthr in (("fixed", 0, 0), ("lat", 1 << 62, 0), ("chainfixed", 1 << 62, 1 << 62)):
+            if mode == "chainfixed" and n > 256:
+                continue
             bt.set_latency_batch(thr)
+            bt.set_chain_batch(cthr)
             res = []
             for _ in range(max(3, args.reps // 2) + 1):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -158,6 +162,7 @@ def main():
             med = statistics.median(res[1:])
             emit(f"batch_{n}_{mode}", res[1:], {"chunks": n, "GiB_per_s": round(n * CHUNK / med / 2**30, 2)})
     bt.set_latency_batch(prev)
+    bt.set_chain_batch(prev_chain_fixed)
     # The same chunks as ragged messages through the chain kernel (one
     # two-wave workgroup per chunk).
     bt.set_chain_batch(1 << 62)

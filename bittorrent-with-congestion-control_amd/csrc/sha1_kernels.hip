@@ -575,31 +575,9 @@ __device__ __forceinline__ void rounds_wk_regs(uint32_t &a, uint32_t &b, uint32_
   }
 }
 
-// Rounds of one block from registers `cur` while the next block's words are
-// read into `nxt`, one 16-byte broadcast read per 4 rounds: the reads are
-// spread over the block (never more than a few in flight, so no wait for the
-// LDS queue) and the block starts with the single wait that covers them all.
-template <int G>
-__device__ __forceinline__ void rounds_prefetch(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
-                                                const u32x4 (&cur)[20], u32x4 (&nxt)[20], const u32x4 *slot,
-                                                uint32_t knext) {
-  if constexpr (G < 20) {
-    nxt[G] = slot[G * kChainBatch + knext];
-    const u32x4 v = cur[G];
-    round_wk<4 * G>(a, b, c, d, e, v.x);
-    round_wk<4 * G + 1>(a, b, c, d, e, v.y);
-    round_wk<4 * G + 2>(a, b, c, d, e, v.z);
-    round_wk<4 * G + 3>(a, b, c, d, e, v.w);
-    __builtin_amdgcn_sched_barrier(0);
-    rounds_prefetch<G + 1>(a, b, c, d, e, cur, nxt, slot, knext);
-  }
-}
-
-__device__ __forceinline__ void chain_rounds(State &st, const u32x4 (&cur)[20], u32x4 (&nxt)[20], const u32x4 *slot,
-                                             uint32_t knext) {
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): `cur` has landed
+__device__ __forceinline__ void chain_rounds(State &st, const u32x4 (&q)[20]) {
   uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
-  rounds_prefetch<0>(a, b, c, d, e, cur, nxt, slot, knext);
+  rounds_wk_regs<0>(a, b, c, d, e, q);
   st.h0 += a;  // sha.c:446-450
   st.h1 += b;
   st.h2 += c;
@@ -662,10 +640,14 @@ __global__ __launch_bounds__(128) void k_sha1_chain(const uint8_t *__restrict__ 
       // never wait on LDS and the loop carries one lgkmcnt wait per block.
       u32x4 wa[20], wb[20];
       chain_fetch(wa, slot, 0);
-      for (uint32_t k = 0; k < nb; k += 2) {  // prefetch indices clamp to the batch's last block
-        chain_rounds(st, wa, wb, slot, k + 1 < nb ? k + 1 : nb - 1);
-        if (k + 1 < nb) chain_rounds(st, wb, wa, slot, k + 2 < nb ? k + 2 : nb - 1);
+      uint32_t k = 0;
+      for (; k + 2 <= nb; k += 2) {
+        chain_fetch(wb, slot, k + 1);
+        chain_rounds(st, wa);
+        chain_fetch(wa, slot, k + 2 < nb ? k + 2 : nb - 1);
+        chain_rounds(st, wb);
       }
+      if (k < nb) chain_rounds(st, wa);
       BT_LAT_BARRIER(nbar);
     }
     BT_LAT_CHECK(nbar, nbatch + 1u);

@@ -434,7 +434,7 @@ def main():
                 "kernel": kernel, "kernel_ms": round(kern_max, 4),
                 "algorithmic_bytes_per_launch": bytes_per_launch, "traffic_source": traffic_note,
             },
-            "valu_roofline": {
+            "valu_roofline": None if kernel != "k_sha1_fixed" else {
                 "bound": "valu", "achieved": round(valu_tops, 2), "unit": "T int32 lane-ops/s",
                 "peak": round(VALU_MIX_PEAK_TOPS, 2), "frac": round(valu_tops / VALU_MIX_PEAK_TOPS, 4),
                 "peak_at_measured_clock": round(peak_at_clock, 2) if peak_at_clock else None,

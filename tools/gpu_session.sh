@@ -63,8 +63,11 @@ for step in "$@"; do
         done
       done ;;
     dist2)
-      run dist2_gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-        --master-port 29531 bench.py --gpus 2 --backend gloo --chunks 8192 --steps 5 --warmup 2 --no-cpu-baseline ;;
+      # the driver's N>1 launch line, rehearsed with 2 and 4 ranks sharing this box's one GPU
+      run dist2 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29531 bench.py --gpus 2 --chunks 16384 --steps 5 --warmup 2
+      run dist4 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+        --master-port 29532 bench.py --gpus 4 --chunks 8192 --steps 5 --warmup 2 ;;
     pairing)
       run pairing 300 "$ROOT/tools/ubench/pairing"
       mkdir -p "$OUT/pairing_pmc"

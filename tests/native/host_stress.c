@@ -1,6 +1,7 @@
 /*
  * tests/native/host_stress.c -- host-side stress of libbtsha1's C runtime
- * (verifier slot ring, host pipelines, streaming drop-in API), built with
+ * (verifier slot ring, host pipelines incl. the worker-list split, streaming
+ * drop-in API), built with
  * host AddressSanitizer/UBSan against an ASan build of the library
  * (`make asan`).  GPU code is not instrumented (not available on this pool).
  * Digests are cross-checked between independent library paths and against
@@ -75,6 +76,12 @@ int main(int argc, char **argv) {
     CHECK(bt_sha1_chunks_host(img, total, cl, a) == (int64_t)n, "chunks_host count");
     CHECK(bt_sha1_chunks_host_multi(img, total, cl, b, 0) == (int64_t)n, "chunks_host_multi count");
     CHECK(!memcmp(a, b, 20 * n), "host vs multi");
+    /* explicit worker list with repeats: 1..8 workers on device 0 */
+    int devs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    memset(b, 0, 20 * n);
+    CHECK(bt_sha1_chunks_host_devices(img, total, cl, b, devs, 1 + t) == (int64_t)n, "chunks_host_devices count: %s",
+          bt_sha1_last_error());
+    CHECK(!memcmp(a, b, 20 * n), "host vs device list (%d workers)", 1 + t);
     uint8_t d[20];
     shahash(img + (n - 1) * cl, (int)(total - (n - 1) * cl), d);
     CHECK(!memcmp(d, a + 20 * (n - 1), 20), "short tail");

@@ -367,7 +367,10 @@ __device__ __forceinline__ void consume_wk(uint32_t &a, uint32_t &b, uint32_t &c
   }
 }
 
-template <int T, int TEND>
+// W+K of rounds T..TEND-1 into an LDS slot: 16-byte entry (T/4) of lane's
+// block at slot[(T/4)*QS + lane*LS].  k_sha1_lat: QS = 64, LS = 1 (word-major,
+// one chunk per lane); k_sha1_chain: QS = 1, LS = kChainStride (block-major).
+template <int T, int TEND, int QS = 64, int LS = 1>
 __device__ __forceinline__ void produce_wk(uint32_t (&w)[16], u32x4 *slot, uint32_t lane) {
   if constexpr (T < TEND) {
     u32x4 q;
@@ -375,8 +378,8 @@ __device__ __forceinline__ void produce_wk(uint32_t (&w)[16], u32x4 *slot, uint3
     q.y = sched<T + 1>(w) + kconst<T + 1>();
     q.z = sched<T + 2>(w) + kconst<T + 2>();
     q.w = sched<T + 3>(w) + kconst<T + 3>();
-    slot[(T / 4) * 64 + lane] = q;
-    produce_wk<T + 4, TEND>(w, slot, lane);
+    slot[(T / 4) * QS + lane * LS] = q;
+    produce_wk<T + 4, TEND, QS, LS>(w, slot, lane);
   }
 }
 
@@ -555,29 +558,39 @@ __device__ __forceinline__ void chain_block(uint32_t (&w)[16], const uint8_t *p,
   }
 }
 
-// R side of the chain kernel: one block's W+K words from an LDS slot
-// (broadcast: every lane reads the same 16 bytes) and the 80 rounds on them.
-__device__ __forceinline__ void chain_fetch(u32x4 (&q)[20], const u32x4 *slot, uint32_t k) {
-#pragma unroll
-  for (int j = 0; j < 20; ++j) q[j] = slot[j * kChainBatch + k];
+// R side of the chain kernel.  A slot holds 64 blocks block-major: block k's
+// 80 W+K words are 20 16-byte entries at slot[k*kChainStride ..] (stride 21:
+// S's 64 lanes then write to spread banks).  R needs one word per round, and
+// its 64 lanes all run the same chain, so instead of broadcasting every word
+// to every lane (20 ds_read_b128 per block) lane L < 16 reads words 4L..4L+3
+// and lane L < 4 words 64+4L..64+4L+3 -- two ds_read_b128 per block -- and
+// round t takes its word from lane t/4 through a DPP row shift folded into
+// the round's add (v_add_u32_dpp ... row_shl:t/4).  Lane 0 therefore runs
+// the exact chain (sha.c:57-64) and owns the result; the other lanes compute
+// garbage.  tools/ubench/chain_floor: 5.99 ms per 512 KiB chain against 6.26
+// for the broadcast form and 5.65 for the same rounds with no loads at all.
+constexpr uint32_t kChainStride = 21;
+
+template <int T>
+__device__ __forceinline__ uint32_t wk_from_lane(const u32x4 &A, const u32x4 &B) {
+  constexpr int g = T < 64 ? T / 4 : (T - 64) / 4;
+  const uint32_t src = T < 64 ? A[T % 4] : B[T % 4];
+  if constexpr (g == 0) return src;
+  else return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)src, 0x100 + g, 0xF, 0xF, false);  // row_shl:g
 }
 
 template <int T>
-__device__ __forceinline__ void rounds_wk_regs(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
-                                               const u32x4 (&q)[20]) {
+__device__ __forceinline__ void chain_rounds_from(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
+                                                  const u32x4 &A, const u32x4 &B) {
   if constexpr (T < 80) {
-    const u32x4 v = q[T / 4];
-    round_wk<T>(a, b, c, d, e, v.x);
-    round_wk<T + 1>(a, b, c, d, e, v.y);
-    round_wk<T + 2>(a, b, c, d, e, v.z);
-    round_wk<T + 3>(a, b, c, d, e, v.w);
-    rounds_wk_regs<T + 4>(a, b, c, d, e, q);
+    round_wk<T>(a, b, c, d, e, wk_from_lane<T>(A, B));
+    chain_rounds_from<T + 1>(a, b, c, d, e, A, B);
   }
 }
 
-__device__ __forceinline__ void chain_rounds(State &st, const u32x4 (&q)[20]) {
+__device__ __forceinline__ void chain_rounds(State &st, const u32x4 &A, const u32x4 &B) {
   uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
-  rounds_wk_regs<0>(a, b, c, d, e, q);
+  chain_rounds_from<0>(a, b, c, d, e, A, B);
   st.h0 += a;  // sha.c:446-450
   st.h1 += b;
   st.h2 += c;
@@ -591,7 +604,7 @@ __global__ __launch_bounds__(128) void k_sha1_chain(const uint8_t *__restrict__ 
                                                     uint64_t tail_len, uint32_t *__restrict__ state,
                                                     uint8_t *__restrict__ digests, const uint8_t *__restrict__ expected,
                                                     uint8_t *__restrict__ ok) {
-  __shared__ u32x4 lds[2][20 * kChainBatch];  // 2 slots x 64 blocks x 80 W+K words = 40 KiB
+  __shared__ u32x4 lds[2][kChainStride * kChainBatch];  // 2 slots x 64 blocks x (80 + 4) words = 42 KiB
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t i = blockIdx.x;
@@ -610,7 +623,7 @@ __global__ __launch_bounds__(128) void k_sha1_chain(const uint8_t *__restrict__ 
       const uint64_t g = bt * kChainBatch + lane;
       uint32_t w[16];
       chain_block<MID>(w, p, g < nb_total ? g : nb_total, nfull, r, len * 8ull);
-      produce_wk<0, 80>(w, lds[bt & 1u], lane);
+      produce_wk<0, 80, 1, kChainStride>(w, lds[bt & 1u], lane);
       BT_LAT_BARRIER(nbar);
     }
     BT_LAT_BARRIER(nbar);  // pairs with R's last barrier
@@ -623,31 +636,21 @@ __global__ __launch_bounds__(128) void k_sha1_chain(const uint8_t *__restrict__ 
     } else {
       st.init();
     }
-    // R's 64 lanes run the same chain off broadcast LDS reads, so every value
-    // is uniform; left alone, hipcc proves that, keeps the chaining state in
-    // SGPRs and pays v_readfirstlane + split adds per block (488 VALU instead
-    // of 405, seen in the ISA).  An opaque zero in a VGPR keeps the chain in
-    // VGPRs, where the round is 5 VALU (bitop3, 2 alignbit, add3, add).
-    uint32_t vzero;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
     BT_LAT_BARRIER(nbar);  // batch 0 is in slot 0
+    const uint32_t l16 = lane & 15u, l4 = lane & 3u;
     for (uint64_t bt = 0; bt < nbatch; ++bt) {
-      const u32x4 *slot = lds[bt & 1u] + vzero;
+      const u32x4 *slot = lds[bt & 1u];
       const uint64_t left = nb_total - bt * kChainBatch;
       const uint32_t nb = left < kChainBatch ? (uint32_t)left : kChainBatch;
-      // Two register buffers of a block's 80 W+K words: block k+1 is read
-      // (broadcast ds_read_b128) while block k's rounds run, so the rounds
-      // never wait on LDS and the loop carries one lgkmcnt wait per block.
-      u32x4 wa[20], wb[20];
-      chain_fetch(wa, slot, 0);
-      uint32_t k = 0;
-      for (; k + 2 <= nb; k += 2) {
-        chain_fetch(wb, slot, k + 1);
-        chain_rounds(st, wa);
-        chain_fetch(wa, slot, k + 2 < nb ? k + 2 : nb - 1);
-        chain_rounds(st, wb);
+      // Block k+1's two reads are issued before block k's rounds.
+      u32x4 A = slot[l16], B = slot[16 + l4];
+      for (uint32_t k = 0; k < nb; ++k) {
+        const u32x4 *nxt = slot + (k + 1 < nb ? k + 1 : k) * kChainStride;
+        const u32x4 An = nxt[l16], Bn = nxt[16 + l4];
+        chain_rounds(st, A, B);
+        A = An;
+        B = Bn;
       }
-      if (k < nb) chain_rounds(st, wa);
       BT_LAT_BARRIER(nbar);
     }
     BT_LAT_CHECK(nbar, nbatch + 1u);

@@ -156,3 +156,24 @@ def test_latency_kernel_loader_ring_keeps_loads_in_flight(asm):
     waits = _first_wait_after_each_load_group(text, LAT_SYM, load="buffer_load_dwordx4")
     assert waits, "no buffer load groups found"
     assert min(waits) >= 4, waits
+
+
+CHAIN_SYM = "_ZN6btsha112k_sha1_chainILb0ELb0EEEvPKhPKmPKjmmmPjPhS2_S8_"
+
+
+def test_chain_kernel_round_wave_structure(asm):
+    """k_sha1_chain's round wave: per block two ds_read_b128
+    (lanes 0..15 / 0..3 hold the block's 80 W+K words) and one add per round
+    fed by a DPP row shift from the lane that holds the word, so the loop is
+    ~405 VALU with no per-round LDS traffic (the broadcast form had 20
+    ds_read_b128 and ~8 waits per block)."""
+    import collections
+    _, text = asm
+    loops = [b for _, b in _loops(text, CHAIN_SYM) if "v_alignbit_b32" in b]
+    assert len(loops) == 1, len(loops)
+    ops = collections.Counter(l.strip().split()[0] for l in loops[0].splitlines()
+                              if l.strip() and not l.strip().startswith((".", ";")))
+    valu = sum(v for k, v in ops.items() if k.startswith("v_"))
+    assert 405 <= valu <= 410, ops
+    assert ops["ds_read_b128"] == 2 and ops["v_add_u32_dpp"] >= 70, ops
+    assert ops["v_alignbit_b32"] == 160 and ops["v_bitop3_b32"] == 80, ops

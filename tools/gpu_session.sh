@@ -73,6 +73,7 @@ for step in "$@"; do
       mkdir -p "$OUT/pairing_pmc"
       run pairing_pmc 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pairing_pmc" -o p -- "$ROOT/tools/ubench/pairing" ;;
     vgprbank) run vgprbank 300 "$ROOT/tools/ubench/vgprbank" ;;
+    chain_floor) run chain_floor 300 "$ROOT/tools/ubench/chain_floor" ;;
     order_pmc)
       # co-issue counters per instruction order of the block (compute only)
       mkdir -p "$OUT/order_pmc"

@@ -121,7 +121,8 @@ def _loops(text, sym):
     body = text[text.index(sym + ":"):]
     body = body[:body.index(".Lfunc_end")]
     out = []
-    for m in re.finditer(r"^(\.LBB\d+_\d+):[^\n]*Inner Loop Header", body, re.M):
+    # the header comment sits on the label's line or, for nested loops, the next one
+    for m in re.finditer(r"^(\.LBB\d+_\d+):[^\n]*(?:\n\s*;[^\n]*)?Inner Loop Header", body, re.M):
         label = m.group(1)
         end = re.search(r"s_cbranch_\w+ " + re.escape(label) + r"\b", body[m.end():])
         if end:  # loops entered by fall-through from a latch block are not innermost-simple

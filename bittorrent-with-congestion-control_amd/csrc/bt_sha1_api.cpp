@@ -131,6 +131,7 @@ struct DevCtx {
   hipStream_t s = nullptr;  // drop-in calls and NULL-stream launches (= lane[0].s)
   Lane lane[2];
   PinBuf h_msg, h_state;  // drop-in calls: message / chaining state, read and written by the chain kernel
+  uint32_t seq = 0;       // drop-in calls: completion word the chain kernel stores at h_state + 32
 };
 
 std::mutex g_ctx_mu;
@@ -546,6 +547,43 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
   return n;
 }
 
+// Wait for a drop-in call's chain kernel: spin on the completion word it
+// stores into pinned memory after its results (a stream wait sleeps and wakes
+// late; ~354 such waits per chunk in SHA1Update's packet-sized calls).  The
+// stream is polled too, so an error or a kernel that ended without the word
+// cannot hang the caller.  BT_SHA1_SYNC=stream waits on the stream instead.
+bool spin_sync() {
+  static const bool on = [] {
+    const char *e = getenv("BT_SHA1_SYNC");
+    return !(e && !strcmp(e, "stream"));
+  }();
+  return on;
+}
+
+int wait_chain(DevCtx *c, const volatile uint32_t *done, uint32_t seq) {
+  if (!spin_sync()) {
+    BT_CK(hipStreamSynchronize(c->s));
+    return 0;
+  }
+  for (uint32_t it = 0;; ++it) {
+    if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == seq) return 0;
+    if ((it & 63u) == 63u) {
+      const hipError_t q = hipStreamQuery(c->s);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == seq) return 0;
+        set_err("chain kernel finished without its completion word");
+        return -1;
+      }
+      if (q != hipErrorNotReady) {
+        set_err("chain kernel: %s", hipGetErrorString(q));
+        return -1;
+      }
+    }
+  }
+}
+
+uint32_t *done_word(DevCtx *c) { return reinterpret_cast<uint32_t *>(c->h_state.as<uint8_t>() + 32); }
+
 // Single message on the GPU (shahash): copy it into the context's pinned
 // staging buffer and launch the chain kernel on it there -- the kernel reads
 // the message over PCIe itself (64 blocks per load batch, far ahead of the
@@ -556,8 +594,10 @@ int hash_one(DevCtx *c, const uint8_t *buf, uint32_t len, uint8_t out[20]) {
   if (ensure_streams(c)) return -1;
   if (c->h_msg.ensure((size_t)len + 64) || c->h_state.ensure(64)) return -1;
   if (len) memcpy(c->h_msg.p, buf, len);
-  BT_CK(btsha1_launch_chain(c->h_msg.p, nullptr, nullptr, 0, len, 1, c->h_state.as<uint8_t>(), c->s));
-  BT_CK(hipStreamSynchronize(c->s));
+  const uint32_t seq = ++c->seq;
+  *done_word(c) = seq - 1u;
+  BT_CK(btsha1_launch_chain_one(c->h_msg.p, len, c->h_state.as<uint8_t>(), c->s, done_word(c), seq));
+  if (wait_chain(c, done_word(c), seq)) return -1;
   memcpy(out, c->h_state.p, 20);
   return 0;
 }
@@ -576,8 +616,10 @@ int midstate(DevCtx *c, uint32_t h[5], const uint8_t *head, const uint8_t *block
   if (nblocks) memcpy(dst + (head ? 64 : 0), blocks, (size_t)nblocks * 64);
   memcpy(c->h_state.p, h, 20);
   nblocks = total;
-  BT_CK(btsha1_launch_chain_midstate(c->h_state.as<uint32_t>(), c->h_msg.p, nblocks, c->s));
-  BT_CK(hipStreamSynchronize(c->s));
+  const uint32_t seq = ++c->seq;
+  *done_word(c) = seq - 1u;
+  BT_CK(btsha1_launch_chain_midstate(c->h_state.as<uint32_t>(), c->h_msg.p, nblocks, c->s, done_word(c), seq));
+  if (wait_chain(c, done_word(c), seq)) return -1;
   memcpy(h, c->h_state.p, 20);
   return 0;
 }

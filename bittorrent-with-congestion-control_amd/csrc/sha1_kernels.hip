@@ -603,7 +603,8 @@ __global__ __launch_bounds__(128) void k_sha1_chain(const uint8_t *__restrict__ 
                                                     const uint32_t *__restrict__ lens, uint64_t pitch, uint64_t fixed_len,
                                                     uint64_t tail_len, uint32_t *__restrict__ state,
                                                     uint8_t *__restrict__ digests, const uint8_t *__restrict__ expected,
-                                                    uint8_t *__restrict__ ok) {
+                                                    uint8_t *__restrict__ ok, uint32_t *__restrict__ done,
+                                                    uint32_t seq) {
   __shared__ u32x4 lds[2][kChainStride * kChainBatch];  // 2 slots x 64 blocks x (80 + 4) words = 42 KiB
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -677,6 +678,9 @@ __global__ __launch_bounds__(128) void k_sha1_chain(const uint8_t *__restrict__ 
           ok[i] = diff == 0;
         }
       }
+      // Completion word for a host that spins instead of waiting on the
+      // stream (drop-in calls): released at system scope after the results.
+      if (done) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -1055,10 +1059,18 @@ hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_
   return hipGetLastError();
 }
 
-hipError_t btsha1_launch_chain_midstate(uint32_t *state, const void *data, uint64_t nblocks, hipStream_t s) {
+hipError_t btsha1_launch_chain_midstate(uint32_t *state, const void *data, uint64_t nblocks, hipStream_t s,
+                                        uint32_t *done, uint32_t seq) {
   if (nblocks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sha1_chain<true>, dim3(1), dim3(128), 0, s, (const uint8_t *)data, nullptr, nullptr, 0ull,
-                     nblocks * 64ull, 0ull, state, nullptr, nullptr, nullptr);
+                     nblocks * 64ull, 0ull, state, nullptr, nullptr, nullptr, done, seq);
+  return hipGetLastError();
+}
+
+hipError_t btsha1_launch_chain_one(const void *msg, uint64_t len, uint8_t *digest, hipStream_t s, uint32_t *done,
+                                   uint32_t seq) {
+  hipLaunchKernelGGL((k_sha1_chain<false, false>), dim3(1), dim3(128), 0, s, (const uint8_t *)msg, nullptr, nullptr,
+                     0ull, len, 0ull, nullptr, digest, nullptr, nullptr, done, seq);
   return hipGetLastError();
 }
 
@@ -1070,10 +1082,10 @@ hipError_t btsha1_launch_chain(const void *base, const uint64_t *offsets, const 
   if (grid > 0x7fffffffull || (ok && (offsets || tail_len))) return hipErrorInvalidValue;
   if (ok)
     hipLaunchKernelGGL((k_sha1_chain<false, true>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)base, offsets,
-                       lens, pitch, fixed_len, tail_len, nullptr, digests, expected, ok);
+                       lens, pitch, fixed_len, tail_len, nullptr, digests, expected, ok, nullptr, 0u);
   else
     hipLaunchKernelGGL((k_sha1_chain<false, false>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)base,
-                       offsets, lens, pitch, fixed_len, tail_len, nullptr, digests, expected, ok);
+                       offsets, lens, pitch, fixed_len, tail_len, nullptr, digests, expected, ok, nullptr, 0u);
   return hipGetLastError();
 }
 

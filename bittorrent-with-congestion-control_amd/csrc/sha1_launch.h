@@ -47,7 +47,13 @@ hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const
 hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_t nblocks, hipStream_t s);
 // Chain kernel (one message per two-wave workgroup; lowest single-chain
 // latency).  state / data may be device or pinned host memory.
-hipError_t btsha1_launch_chain_midstate(uint32_t *state, const void *data, uint64_t nblocks, hipStream_t s);
+// done != NULL: after the results, *done = seq is stored with a system-scope
+// release, so a host can spin on it instead of waiting on the stream.
+hipError_t btsha1_launch_chain_midstate(uint32_t *state, const void *data, uint64_t nblocks, hipStream_t s,
+                                        uint32_t *done = nullptr, uint32_t seq = 0);
+// One message of len bytes at msg (device or pinned host memory), digest to digest.
+hipError_t btsha1_launch_chain_one(const void *msg, uint64_t len, uint8_t *digest, hipStream_t s,
+                                   uint32_t *done = nullptr, uint32_t seq = 0);
 // n messages: message i at base + (offsets ? offsets[i] : i*pitch), length
 // lens ? lens[i] : fixed_len; digest i (big-endian bytes) at digests + 20*i
 // (digests may be NULL with ok).  tail_len != 0 (no offsets): one more message

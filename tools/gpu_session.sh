@@ -175,6 +175,10 @@ for step in "$@"; do
       run stream_prof 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/stream_prof" -o sb \
         -- python3 "$ROOT/tools/stream_bench.py" 4 ;;
     latency) run latency 300 python3 tools/latency_bench.py ;;
+    latency_ab)
+      run latency_spin 300 python3 tools/latency_bench.py
+      run latency_streamsync 300 env BT_SHA1_SYNC=stream python3 tools/latency_bench.py
+      run latency_spin2 300 python3 tools/latency_bench.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1030,13 +1030,16 @@ const char *btsha1_fixed_kernel_name(uint64_t n, int variant) {
 }
 
 // Ragged batches of at most this many messages take the chain kernel (one
-// two-wave workgroup per message; 0: never).  Default: one per CU.
+// two-wave workgroup per message; 0: never).  Default: two per CU -- three
+// 42 KiB workgroups fit a CU's LDS, and at 2 per CU a lone chain still takes
+// 6.07 ms vs 6.71 in k_sha1_lat; at 4 per CU the second round of workgroups
+// costs 17.8 ms (tools/latency_bench.py, profiles/r02/latency.txt).
 static uint64_t g_chain_max = BT_SHA1_CHAIN_AUTO;
 void btsha1_set_chain_batch(uint64_t max_messages) { __atomic_store_n(&g_chain_max, max_messages, __ATOMIC_RELAXED); }
 uint64_t btsha1_chain_batch_setting() { return __atomic_load_n(&g_chain_max, __ATOMIC_RELAXED); }
 uint64_t btsha1_chain_batch() {
   const uint64_t v = btsha1_chain_batch_setting();
-  return v == BT_SHA1_CHAIN_AUTO ? (uint64_t)btsha1_device_cus() : v;
+  return v == BT_SHA1_CHAIN_AUTO ? 2ull * btsha1_device_cus() : v;
 }
 
 hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t pitch,

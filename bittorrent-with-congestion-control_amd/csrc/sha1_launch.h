@@ -29,7 +29,7 @@ const char *btsha1_fixed_kernel_name(uint64_t n, int variant);
 void btsha1_set_latency_batch(uint64_t max_chunks);
 uint64_t btsha1_latency_batch_setting();  // raw setting (may be BT_SHA1_LATENCY_AUTO)
 uint64_t btsha1_latency_batch();          // effective threshold on the current device
-#define BT_SHA1_CHAIN_AUTO UINT64_MAX  // = CUs of the launching device
+#define BT_SHA1_CHAIN_AUTO UINT64_MAX  // = 2 x CUs of the launching device
 void btsha1_set_chain_batch(uint64_t max_messages);
 uint64_t btsha1_chain_batch_setting();
 uint64_t btsha1_chain_batch();

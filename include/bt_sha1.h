@@ -71,7 +71,7 @@ uint64_t bt_sha1_set_latency_batch(uint64_t max_chunks);
  * message, the lowest latency a single serial chain gets (shahash and the
  * SHA1Update/SHA1Final midstate always use it); larger batches the
  * one-message-per-lane ragged kernel.  0 disables it; UINT64_MAX (default) =
- * one per compute unit.  Returns the previous setting. */
+ * two per compute unit.  Returns the previous setting. */
 uint64_t bt_sha1_set_chain_batch(uint64_t max_messages);
 /* Name of the kernel a fixed-layout batch of n_chunks chunks runs on the
  * current device ("k_sha1_fixed", "k_sha1_lat" or "k_sha1_lds"); NULL without

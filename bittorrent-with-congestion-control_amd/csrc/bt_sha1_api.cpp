@@ -551,7 +551,9 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
 // stores into pinned memory after its results (a stream wait sleeps and wakes
 // late; ~354 such waits per chunk in SHA1Update's packet-sized calls).  The
 // stream is polled too, so an error or a kernel that ended without the word
-// cannot hang the caller.  BT_SHA1_SYNC=stream waits on the stream instead.
+// cannot hang the caller, and after 1 ms the wait blocks on the stream instead
+// (long messages do not burn a core; the wake-up latency is then noise).
+// BT_SHA1_SYNC=stream always waits on the stream.
 bool spin_sync() {
   static const bool on = [] {
     const char *e = getenv("BT_SHA1_SYNC");
@@ -565,8 +567,15 @@ int wait_chain(DevCtx *c, const volatile uint32_t *done, uint32_t seq) {
     BT_CK(hipStreamSynchronize(c->s));
     return 0;
   }
+  const double t0 = now_s();
   for (uint32_t it = 0;; ++it) {
     if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == seq) return 0;
+    if ((it & 1023u) == 1023u && now_s() - t0 > 1e-3) {
+      BT_CK(hipStreamSynchronize(c->s));
+      if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == seq) return 0;
+      set_err("chain kernel finished without its completion word");
+      return -1;
+    }
     if ((it & 63u) == 63u) {
       const hipError_t q = hipStreamQuery(c->s);
       if (q == hipSuccess) {

@@ -13,8 +13,8 @@
 //                   line offset rides in the scalar soffset -> zero VALU
 //                   address arithmetic in the loop.
 //   k_sha1_lds      the hot path with coalesced LDS-DMA staging (a variant).
-//   k_sha1_lat      small fixed-layout batches (<= 64 chunks per CU, 16384 on
-//                   MI355X: shahash, small verify batches): a loader/schedule wave and a round
+//   k_sha1_lat      small fixed-layout batches (<= 128 chunks per CU, 32768 on
+//                   MI355X: small verify batches): a loader/schedule wave and a round
 //                   wave per 64 chunks meet in LDS, cutting a lone chain's
 //                   instruction count from 597 to ~426 per block.
 //   k_sha1_ragged   arbitrary (offset, length) messages and layouts the
@@ -386,8 +386,8 @@ __device__ __forceinline__ void produce_wk(uint32_t (&w)[16], u32x4 *slot, uint3
 // Barrier accounting of k_sha1_lat.  S and R run different code, so the
 // workgroup barrier is met from different call sites; s_barrier counts WAVES,
 // and the kernel is correct only while both waves execute exactly the same
-// number of barriers: nb_total + 1 each (S: one per produced block + one
-// final; R: one before its loop + one per consumed block).  Any edit that
+// number of barriers: nb_total + SLOTS - 1 each (S: one per produced block +
+// SLOTS - 1 final; R: SLOTS - 1 before its loop + one per consumed block).  Any edit that
 // changes one side's block count deadlocks the workgroup silently.  Build
 // with -DBT_SHA1_DEBUG_BARRIERS to count them per wave and trap on a mismatch.
 #ifdef BT_SHA1_DEBUG_BARRIERS
@@ -405,20 +405,56 @@ __device__ __forceinline__ void produce_wk(uint32_t (&w)[16], u32x4 *slot, uint3
 #define BT_LAT_CHECK(cnt, want) ((void)0)
 #endif
 
-// One block through S into slot p, then the block's barrier.
+// One block through S into slot p of SLOTS, then the block's barrier.
+template <int SLOTS>
 __device__ __forceinline__ void produce_block(uint32_t (&w)[16], u32x4 (*lds)[20 * 64], uint32_t &p, uint32_t lane,
                                               uint32_t &nbar) {
   produce_wk<0, 80>(w, lds[p], lane);
-  p ^= 1u;
+  p = p + 1u == (uint32_t)SLOTS ? 0u : p + 1u;
   BT_LAT_BARRIER(nbar);
 }
 
-template <bool VERIFY>
+template <int T>
+__device__ __forceinline__ void rounds_wk_regs(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
+                                               const u32x4 (&q)[20]) {
+  if constexpr (T < 80) {
+    const u32x4 v = q[T / 4];
+    round_wk<T>(a, b, c, d, e, v.x);
+    round_wk<T + 1>(a, b, c, d, e, v.y);
+    round_wk<T + 2>(a, b, c, d, e, v.z);
+    round_wk<T + 3>(a, b, c, d, e, v.w);
+    rounds_wk_regs<T + 4>(a, b, c, d, e, q);
+  }
+}
+
+// R of k_sha1_lat<.., 3>: one block's 80 W+K words of this lane's chunk from a
+// slot (lane-major 16-byte entries), and the 80 rounds on them.
+__device__ __forceinline__ void lat_fetch(u32x4 (&q)[20], const u32x4 *slot, uint32_t lane) {
+#pragma unroll
+  for (int j = 0; j < 20; ++j) q[j] = slot[j * 64 + lane];
+}
+
+__device__ __forceinline__ void lat_rounds(State &st, const u32x4 (&q)[20]) {
+  uint32_t a = st.h0, b = st.h1, c = st.h2, d = st.h3, e = st.h4;
+  rounds_wk_regs<0>(a, b, c, d, e, q);
+  st.h0 += a;  // sha.c:446-450
+  st.h1 += b;
+  st.h2 += c;
+  st.h3 += d;
+  st.h4 += e;
+}
+
+// SLOTS = 2: S one block ahead (40 KiB of LDS) -- the fastest form while
+// each CU holds one workgroup.  SLOTS = 3: S two blocks ahead and R reading
+// the next block into registers during the current one (60 KiB, so at most
+// two workgroups per CU): it keeps the latency when two workgroups share a
+// CU and their waves share SIMDs (32768 chunks: 6.8 ms vs 11.3 ms).
+template <bool VERIFY, int SLOTS = 2>
 __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ base, uint64_t n_chunks, uint32_t pitch,
                                                   uint32_t len, uint8_t *__restrict__ digests,
                                                   const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok,
                                                   uint32_t tail_len) {
-  __shared__ u32x4 lds[2][20 * 64];  // 2 slots x 80 words x 64 lanes = 40 KiB
+  __shared__ u32x4 lds[SLOTS][20 * 64];  // SLOTS x 80 words x 64 lanes = SLOTS x 20 KiB
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint64_t chunk0 = (uint64_t)blockIdx.x * 64u;  // workgroup-uniform: both waves agree
@@ -433,8 +469,8 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
     len = tail_len;
   }
   const uint32_t nblocks = len >> 6, r = len & 63u;
-  // + MD padding block(s).  Both waves execute nb_total + 1 barriers (see
-  // "Barrier accounting" above).
+  // + MD padding block(s).  Both waves execute nb_total + SLOTS - 1 barriers
+  // (see "Barrier accounting" above).
   const uint32_t nb_total = nblocks + (r >= 56u ? 2u : 1u);
   uint32_t nbar = 0;
   (void)nbar;
@@ -449,7 +485,7 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
     // pace): S must never stall on memory, or R waits at the barrier.  Loads
     // past nrec are range-checked zeros, so they need no guard (and no branch
     // that would make the compiler wait for them, see absorb_ring).
-    uint32_t slot = 0;
+    uint32_t slot = 0;  // LDS slot the next block goes to
     u32x4 ring[4][4];
 #pragma unroll
     for (int k = 0; k < 3; ++k)
@@ -465,7 +501,7 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
         if (b + k < nblocks) {  // wave-uniform
           uint32_t w[16];
           block_from_le(w, ring[k][0], ring[k][1], ring[k][2], ring[k][3]);
-          produce_block(w, lds, slot, lane, nbar);
+          produce_block<SLOTS>(w, lds, slot, lane, nbar);
         }
       }
     }
@@ -477,31 +513,58 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
     for (int j = 0; j < 16; ++j) tail[j] |= (j == (int)wi) ? mark : 0u;
     const uint64_t bits = (uint64_t)len * 8ull;
     if (r >= 56u) {
-      produce_block(tail, lds, slot, lane, nbar);
+      produce_block<SLOTS>(tail, lds, slot, lane, nbar);
 #pragma unroll
       for (int j = 0; j < 16; ++j) tail[j] = 0u;
     }
     tail[14] = (uint32_t)(bits >> 32);
     tail[15] = (uint32_t)bits;
-    produce_block(tail, lds, slot, lane, nbar);
-    BT_LAT_BARRIER(nbar);  // pairs with R's last barrier
-    BT_LAT_CHECK(nbar, nb_total + 1u);
+    produce_block<SLOTS>(tail, lds, slot, lane, nbar);
+#pragma unroll
+    for (int k = 0; k < SLOTS - 1; ++k) BT_LAT_BARRIER(nbar);  // pair with R's last barriers
+    BT_LAT_CHECK(nbar, nb_total + SLOTS - 1u);
   } else {
     // ---- R: rounds -----------------------------------------------------------
     State st;
     st.init();
-    BT_LAT_BARRIER(nbar);  // block 0 is in slot 0
-    for (uint32_t b = 0; b < nb_total; ++b) {
-      uint32_t a = st.h0, bb = st.h1, c = st.h2, d = st.h3, e = st.h4;
-      consume_wk<0, 80>(a, bb, c, d, e, lds[b & 1u], lane);
-      BT_LAT_BARRIER(nbar);
-      st.h0 += a;  // sha.c:446-450
-      st.h1 += bb;
-      st.h2 += c;
-      st.h3 += d;
-      st.h4 += e;
+    if constexpr (SLOTS == 2) {
+      BT_LAT_BARRIER(nbar);  // block 0 is in slot 0
+      for (uint32_t b = 0; b < nb_total; ++b) {
+        uint32_t a = st.h0, bb = st.h1, c = st.h2, d = st.h3, e = st.h4;
+        consume_wk<0, 80>(a, bb, c, d, e, lds[b & 1u], lane);
+        BT_LAT_BARRIER(nbar);
+        st.h0 += a;  // sha.c:446-450
+        st.h1 += bb;
+        st.h2 += c;
+        st.h3 += d;
+        st.h4 += e;
+      }
+    } else {
+      // S runs two blocks ahead: once barrier b+2 has passed, blocks b and
+      // b+1 are both in LDS, so R reads block b+1 into registers while block
+      // b's rounds run.  S overwrites slot (b+2) % 3 = (b-1) % 3 only after
+      // barrier b+2, by which R has consumed block b-1 (its reads completed
+      // before barrier b+1, which waits for them).
+      BT_LAT_BARRIER(nbar);  // block 0 is in
+      BT_LAT_BARRIER(nbar);  // block 1 (or S's first closing barrier) is in
+      u32x4 wa[20], wb[20];
+      lat_fetch(wa, lds[0], lane);
+      uint32_t sb = 0;  // slot of block b
+      for (uint32_t b = 0; b < nb_total; b += 2) {
+        const uint32_t s1 = sb + 1u == 3u ? 0u : sb + 1u;
+        const uint32_t s2 = s1 + 1u == 3u ? 0u : s1 + 1u;
+        lat_fetch(wb, lds[b + 1 < nb_total ? s1 : sb], lane);
+        lat_rounds(st, wa);
+        BT_LAT_BARRIER(nbar);  // block b + 2 is in
+        if (b + 1 < nb_total) {  // wave-uniform
+          lat_fetch(wa, lds[b + 2 < nb_total ? s2 : s1], lane);
+          lat_rounds(st, wb);
+          BT_LAT_BARRIER(nbar);  // block b + 3 is in
+        }
+        sb = s2;
+      }
     }
-    BT_LAT_CHECK(nbar, nb_total + 1u);
+    BT_LAT_CHECK(nbar, nb_total + SLOTS - 1u);
     store_digest<VERIFY>(st, lane, nvalid, chunk0, digests, expected, ok);
   }
 }
@@ -944,16 +1007,28 @@ static hipError_t launch_lds(const void *d_in, uint64_t n, uint32_t pitch, uint3
                        len, d_dig, d_exp, d_ok);
   return hipGetLastError();
 }
+// Up to one workgroup per CU k_sha1_lat runs with two LDS slots; beyond that
+// (two workgroups per CU, whose waves then share SIMDs) with three, where S
+// is two blocks ahead and R never waits on it: 32768 chunks 6.8 ms against
+// 11.3 ms for the two-slot form and 9.1 ms for the hot kernel.  The 60 KiB
+// three-slot workgroup also caps a CU at two of them.
+template <int SLOTS>
+static hipError_t launch_lat_s(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
+                               const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, uint32_t tail_len, uint64_t grid) {
+  if (d_ok)
+    hipLaunchKernelGGL((k_sha1_lat<true, SLOTS>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_in, n,
+                       pitch, len, d_dig, d_exp, d_ok, tail_len);
+  else
+    hipLaunchKernelGGL((k_sha1_lat<false, SLOTS>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_in, n,
+                       pitch, len, d_dig, d_exp, d_ok, tail_len);
+  return hipGetLastError();
+}
+
 static hipError_t launch_lat(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,
                              const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, uint32_t tail_len) {
   const uint64_t grid = (n + 63) / 64 + (tail_len ? 1 : 0);
-  if (d_ok)
-    hipLaunchKernelGGL((k_sha1_lat<true>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_in, n, pitch, len,
-                       d_dig, d_exp, d_ok, tail_len);
-  else
-    hipLaunchKernelGGL((k_sha1_lat<false>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_in, n, pitch, len,
-                       d_dig, d_exp, d_ok, tail_len);
-  return hipGetLastError();
+  return grid > btsha1_device_cus() ? launch_lat_s<3>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s, tail_len, grid)
+                                    : launch_lat_s<2>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s, tail_len, grid);
 }
 
 // Batches of at most this many chunks take the latency kernel (0: never).
@@ -962,7 +1037,7 @@ void btsha1_set_latency_batch(uint64_t max_chunks) { __atomic_store_n(&g_lat_max
 uint64_t btsha1_latency_batch_setting() { return __atomic_load_n(&g_lat_max, __ATOMIC_RELAXED); }
 uint64_t btsha1_latency_batch() {
   const uint64_t v = btsha1_latency_batch_setting();
-  return v == BT_SHA1_LATENCY_AUTO ? (uint64_t)btsha1_device_cus() * 64u : v;
+  return v == BT_SHA1_LATENCY_AUTO ? (uint64_t)btsha1_device_cus() * 128u : v;
 }
 
 constexpr int kLdsVariant = 1010;  // bt_sha1_set_variant(10, 1, 0): LDS-staged k_sha1_lds

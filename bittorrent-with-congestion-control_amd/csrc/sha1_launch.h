@@ -22,9 +22,9 @@ hipError_t btsha1_launch_fixed_stamped(const void *d_in, uint64_t n, uint32_t pi
 const char *btsha1_fixed_kernel_name(uint64_t n, int variant);
 // Batches of at most max_chunks chunks (tail included) take the latency kernel
 // k_sha1_lat instead of the selected variant; 0 disables it.  The default,
-// BT_SHA1_LATENCY_AUTO, is 64 chunks per CU of the launching device (one
-// two-wave workgroup per CU: past that the latency kernel's S and R waves
-// start sharing SIMDs and it loses to the hot kernel).
+// BT_SHA1_LATENCY_AUTO, is 128 chunks per CU of the launching device (at
+// most two two-wave workgroups per CU; past that the latency kernel loses to
+// the hot kernel).
 #define BT_SHA1_LATENCY_AUTO UINT64_MAX
 void btsha1_set_latency_batch(uint64_t max_chunks);
 uint64_t btsha1_latency_batch_setting();  // raw setting (may be BT_SHA1_LATENCY_AUTO)

@@ -62,8 +62,8 @@ int bt_sha1_set_variant(int nbuf, int lines, int nt);
 /* Batches of at most max_chunks chunks take the latency kernel (a loader /
  * schedule wave and a round wave per 64 chunks, meeting in LDS), which
  * shortens a lone chunk's serial chain; larger batches take the hot-kernel
- * variant above.  0 disables it; UINT64_MAX (the default) = 64 chunks per
- * compute unit of the launching device (16384 on a full MI355X).  Returns the
+ * variant above.  0 disables it; UINT64_MAX (the default) = 128 chunks per
+ * compute unit of the launching device (32768 on a full MI355X).  Returns the
  * previous setting. */
 uint64_t bt_sha1_set_latency_batch(uint64_t max_chunks);
 /* Ragged batches (bt_sha1_ragged_dev, strided fallbacks) of at most

@@ -781,7 +781,8 @@ def test_kernel_name_reports_the_launch(bt):
         assert bt.kernel_name(1) == "k_sha1_chain"
         assert bt.kernel_name(512) == "k_sha1_chain"  # two per CU on a 256-CU MI355X
         assert bt.kernel_name(513) == "k_sha1_lat"
-        assert bt.kernel_name(16384) == "k_sha1_lat"  # 64 per CU
+        assert bt.kernel_name(32768) == "k_sha1_lat"  # 128 per CU
+        assert bt.kernel_name(32769) == "k_sha1_fixed"
         assert bt.kernel_name(131072) == "k_sha1_fixed"
         assert "latency_batch=auto" in bt.build_info()
     finally:

@@ -120,7 +120,7 @@ def _sym(text, prefix):
     return found[0]
 
 
-LAT_SYM = "_ZN6btsha110k_sha1_latILb0EE"  # k_sha1_lat<false>
+LAT_SYM = "_ZN6btsha110k_sha1_latILb0ELi2EE"  # k_sha1_lat<false, 2 slots>
 
 
 def _loops(text, sym):

@@ -143,7 +143,7 @@ def main():
             golden[int(i)] = h
     prev = bt.set_latency_batch(0)
     prev_chain_fixed = bt.set_chain_batch(0)
-    for n in (1, 64, 256, 512, 1024, 2048, 4096, 16384, 32768, 65536):
+    for n in (1, 64, 256, 512, 1024, 2048, 4096, 16384, 24576, 32768, 65536):
         for mode, thr, cthr in (("fixed", 0, 0), ("lat", 1 << 62, 0), ("chainfixed", 1 << 62, 1 << 62)):
             if mode == "chainfixed" and n > 4096:
                 continue

@@ -597,8 +597,8 @@ uint32_t *done_word(DevCtx *c) { return reinterpret_cast<uint32_t *>(c->h_state.
 // staging buffer and launch the chain kernel on it there -- the kernel reads
 // the message over PCIe itself (64 blocks per load batch, far ahead of the
 // round wave) and writes the digest straight into pinned memory -- so one
-// synchronous call is one memcpy, one launch and one stream wait: no H2D or
-// D2H copies (each a queue round trip of its own).
+// synchronous call is one memcpy, one launch and a wait on the kernel's
+// completion word: no H2D or D2H copies (each a queue round trip of its own).
 int hash_one(DevCtx *c, const uint8_t *buf, uint32_t len, uint8_t out[20]) {
   if (ensure_streams(c)) return -1;
   if (c->h_msg.ensure((size_t)len + 64) || c->h_state.ensure(64)) return -1;

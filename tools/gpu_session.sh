@@ -164,6 +164,10 @@ for step in "$@"; do
       run vsz_b1024_s4_p256 300 "$VS" -z -b 1024 -s 4 -r 8 -p 256 /tmp/C.tar tests/golden/ref_C.chunks
       run vsz_b4096_s3_p256 300 "$VS" -z -b 4096 -s 3 -r 4 -p 256 /tmp/C.tar tests/golden/ref_C.chunks ;;
     hostpaths) run stream_pageable 600 python3 tools/stream_bench.py 16 && run stream_pageable8 600 python3 tools/stream_bench.py 8 ;;
+    dma_batch)
+      for mb in 1024 2048 4096 1024 2048 4096; do
+        run "dma_batch_$mb" 300 env BT_SHA1_DMA_BATCH_MB=$mb python3 tools/stream_bench.py 8
+      done ;;
     filebench) run filebench 600 env BT_SHA1_TRACE=1 python3 tools/file_bench.py /dev/shm 1 1024 8192 32768 ;;
     vs_prof)
       python3 -c "import lzma; open('/tmp/C.tar','wb').write(lzma.decompress(open('tests/golden/C.tar.xz','rb').read()))"

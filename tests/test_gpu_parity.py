@@ -774,16 +774,19 @@ def test_null_stream_orders_after_default_stream_work(bt, torch, oracle):
         assert int(dig2.sum().item()) == 0, trial
 
 
-def test_kernel_name_reports_the_launch(bt):
+def test_kernel_name_reports_the_launch(bt, torch):
+    """Default thresholds follow the device's CU count (256 on a full MI355X):
+    chain kernel up to 2 chunks per CU, latency kernel up to 128 per CU."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
     lat = bt.set_latency_batch(2**64 - 1)  # auto
     chain = bt.set_chain_batch(2**64 - 1)
     try:
         assert bt.kernel_name(1) == "k_sha1_chain"
-        assert bt.kernel_name(512) == "k_sha1_chain"  # two per CU on a 256-CU MI355X
-        assert bt.kernel_name(513) == "k_sha1_lat"
-        assert bt.kernel_name(32768) == "k_sha1_lat"  # 128 per CU
-        assert bt.kernel_name(32769) == "k_sha1_fixed"
-        assert bt.kernel_name(131072) == "k_sha1_fixed"
+        assert bt.kernel_name(2 * cus) == "k_sha1_chain"
+        assert bt.kernel_name(2 * cus + 1) == "k_sha1_lat"
+        assert bt.kernel_name(128 * cus) == "k_sha1_lat"
+        assert bt.kernel_name(128 * cus + 1) == "k_sha1_fixed"
+        assert bt.kernel_name(131072) == ("k_sha1_fixed" if 128 * cus < 131072 else "k_sha1_lat")
         assert "latency_batch=auto" in bt.build_info()
     finally:
         bt.set_latency_batch(lat)

@@ -858,3 +858,45 @@ def test_streaming_update_pieces_and_context(bt, oracle):
             assert list(s.ctx.hash) == oracle.compress_blocks(
                 [0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476, 0xc3d2e1f0], msg[:done]), k
     assert s.final() == o.final() == oracle.sha1(msg)
+
+
+def test_dropin_calls_from_many_threads(bt, oracle):
+    """shahash / SHA1Update / SHA1Final from several host threads at once (the
+    calls share one device context and its pinned staging; ctypes releases the
+    GIL, so they really overlap) and two SHA1Context streams interleaved on
+    one thread: every digest equals the oracle's."""
+    import threading
+    msgs = [bytes(oracle.fill_synthetic(n, 17 * n, 0x7E57)) for n in (0, 55, 64, 1000, 70000, CHUNK, CHUNK + 3)]
+    want = [oracle.sha1(m) for m in msgs]
+    errors = []
+
+    def worker(k):
+        try:
+            for rep in range(3):
+                for i, m in enumerate(msgs):
+                    if (i + k + rep) % 2:
+                        got = bt.shahash(m)
+                    else:
+                        s = bt.Sha1()
+                        step = 1484 if len(m) > 4096 else 7
+                        for o in range(0, len(m), step):
+                            s.update(m[o:o + step])
+                        got = s.final()
+                    if got != want[i]:
+                        errors.append((k, rep, i))
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:5]
+    # two contexts interleaved
+    a, b = bt.Sha1(), bt.Sha1()
+    ma, mb = msgs[5], msgs[6]
+    for o in range(0, max(len(ma), len(mb)), 4096):
+        a.update(ma[o:o + 4096])
+        b.update(mb[o:o + 4096])
+    assert a.final() == want[5] and b.final() == want[6]

@@ -749,6 +749,152 @@ __global__ __launch_bounds__(128) void k_sha1_chain(const uint8_t *__restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// Latency kernel for RAGGED batches (bt_sha1_ragged_dev with 2 x CUs < n <=
+// 128 x CUs messages): k_sha1_lat's loader / round-wave split with per-lane
+// message pointers and lengths.  Lane j of both waves owns message 64*wg + j;
+// the waves run to the longest message of the 64, lane j latches its state
+// after its own last block.  S reads any alignment (16-byte loads as in
+// SrcBytes) through a four-block register ring; lanes whose message has no
+// whole block read a static zero block instead of running past their message.
+// ---------------------------------------------------------------------------
+__device__ u32x4 kZeroBlock[4];
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+
+template <int SLOTS>
+__global__ __launch_bounds__(128) void k_sha1_lat_ragged(const uint8_t *__restrict__ base,
+                                                         const uint64_t *__restrict__ offsets,
+                                                         const uint32_t *__restrict__ lens, uint64_t pitch,
+                                                         uint32_t fixed_len, uint64_t n, uint8_t *__restrict__ digests) {
+  __shared__ u32x4 lds[SLOTS][20 * 64];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t idx = (uint64_t)blockIdx.x * 64u + lane;
+  const uint64_t mi = idx < n ? idx : n - 1;  // lanes past the end re-hash the last message, no store
+  const uint8_t *p = base + (offsets ? offsets[mi] : mi * pitch);
+  const uint32_t len = lens ? lens[mi] : fixed_len;
+  const uint32_t nfull = len >> 6, r = len & 63u;
+  const uint32_t nb = nfull + (r >= 56u ? 2u : 1u);
+  // Both waves hold the same per-lane lengths, so they agree on the trip count
+  // and on the barrier count: nbmax + SLOTS - 1 each.
+  const uint32_t nbmax = __builtin_amdgcn_readfirstlane(wave_max(nb));
+  uint32_t nbar = 0;
+  (void)nbar;
+  if (wave == 0) {
+    // ---- S -------------------------------------------------------------------
+    const uint8_t *lp = nfull ? p : (const uint8_t *)kZeroBlock;
+    const uint32_t lmax = nfull ? nfull - 1u : 0u;
+    const uint64_t bits = (uint64_t)len * 8ull;
+    // The tail bytes + 0x80 (sha.c:536-538) are read once, up front: a load in
+    // the per-block lane-divergent branch below would make the compiler wait
+    // for the whole prefetch ring at the branch join on every block.
+    uint32_t tw[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) tw[j] = 0u;
+    {
+      const uint8_t *t = p + 64u * nfull;
+      for (uint32_t q = 0; q < r; ++q) tw[q >> 2] |= (uint32_t)t[q] << (24 - 8 * (q & 3));
+      tw[r >> 2] |= 0x80000000u >> ((r & 3) * 8);
+    }
+    uint32_t slot = 0;
+    u32x4 ring[4][4];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) __builtin_memcpy(&ring[k][i], lp + 64u * ((uint32_t)k < lmax ? k : lmax) + 16 * i, 16);
+    for (uint32_t b = 0; b < nbmax; b += 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t nx = b + k + 3u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) __builtin_memcpy(&ring[(k + 3) % 4][i], lp + 64u * (nx < lmax ? nx : lmax) + 16 * i, 16);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t bk = b + k;
+        if (bk < nbmax) {  // wave-uniform
+          uint32_t w[16];
+          if (bk < nfull) {
+            block_from_le(w, ring[k][0], ring[k][1], ring[k][2], ring[k][3]);
+          } else {  // the tail block, then (r >= 56) a length-only block, sha.c:536-543
+#pragma unroll
+            for (int j = 0; j < 16; ++j) w[j] = bk == nfull ? tw[j] : 0u;
+            if ((bk == nfull && r < 56u) || bk == nfull + 1u) {
+              w[14] = (uint32_t)(bits >> 32);
+              w[15] = (uint32_t)bits;
+            }
+          }
+          produce_block<SLOTS>(w, lds, slot, lane, nbar);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SLOTS - 1; ++k) BT_LAT_BARRIER(nbar);  // pair with R's last barriers
+    BT_LAT_CHECK(nbar, nbmax + SLOTS - 1u);
+  } else {
+    // ---- R -------------------------------------------------------------------
+    State st, fin;
+    st.init();
+    fin = st;
+    auto latch = [&](uint32_t b) {  // this lane's last block done: keep its state
+      if (b + 1u == nb) fin = st;
+    };
+    if constexpr (SLOTS == 2) {
+      BT_LAT_BARRIER(nbar);
+      for (uint32_t b = 0; b < nbmax; ++b) {
+        uint32_t a = st.h0, bb = st.h1, c = st.h2, d = st.h3, e = st.h4;
+        consume_wk<0, 80>(a, bb, c, d, e, lds[b & 1u], lane);
+        BT_LAT_BARRIER(nbar);
+        st.h0 += a;  // sha.c:446-450
+        st.h1 += bb;
+        st.h2 += c;
+        st.h3 += d;
+        st.h4 += e;
+        latch(b);
+      }
+    } else {
+      BT_LAT_BARRIER(nbar);
+      BT_LAT_BARRIER(nbar);
+      u32x4 wa[20], wb[20];
+      lat_fetch(wa, lds[0], lane);
+      uint32_t sb = 0;
+      for (uint32_t b = 0; b < nbmax; b += 2) {
+        const uint32_t s1 = sb + 1u == 3u ? 0u : sb + 1u;
+        const uint32_t s2 = s1 + 1u == 3u ? 0u : s1 + 1u;
+        lat_fetch(wb, lds[b + 1 < nbmax ? s1 : sb], lane);
+        lat_rounds(st, wa);
+        latch(b);
+        BT_LAT_BARRIER(nbar);
+        if (b + 1 < nbmax) {
+          lat_fetch(wa, lds[b + 2 < nbmax ? s2 : s1], lane);
+          lat_rounds(st, wb);
+          latch(b + 1);
+          BT_LAT_BARRIER(nbar);
+        }
+        sb = s2;
+      }
+    }
+    BT_LAT_CHECK(nbar, nbmax + SLOTS - 1u);
+    if (idx < n) {
+      uint8_t *o = digests + idx * 20u;
+      const uint32_t h[5] = {fin.h0, fin.h1, fin.h2, fin.h3, fin.h4};
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {  // byte stores: digests need no alignment here
+        o[4 * k] = (uint8_t)(h[k] >> 24);
+        o[4 * k + 1] = (uint8_t)(h[k] >> 16);
+        o[4 * k + 2] = (uint8_t)(h[k] >> 8);
+        o[4 * k + 3] = (uint8_t)h[k];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generic paths (64-bit addressing, any alignment).
 // ---------------------------------------------------------------------------
 // Block source for absorb_ring: how one 64-byte block is fetched into a
@@ -1123,6 +1269,17 @@ hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const
   // A few messages: each one's latency is its serial chain, which the chain
   // kernel runs at ~405 VALU per block instead of the ragged kernel's ~600.
   if (n <= btsha1_chain_batch()) return btsha1_launch_chain(d_base, d_off, d_len, pitch, fixed_len, n, d_dig, s, 0, nullptr, nullptr);
+  // Up to 128 messages per CU: the loader / round-wave split of k_sha1_lat.
+  if (n <= btsha1_latency_batch()) {
+    const uint64_t grid = (n + 63) / 64;
+    if (grid > btsha1_device_cus())
+      hipLaunchKernelGGL(k_sha1_lat_ragged<3>, dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_base, d_off,
+                         d_len, pitch, fixed_len, n, d_dig);
+    else
+      hipLaunchKernelGGL(k_sha1_lat_ragged<2>, dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_base, d_off,
+                         d_len, pitch, fixed_len, n, d_dig);
+    return hipGetLastError();
+  }
   // As launch_fixed_v: below one wave per SIMD, one-wave workgroups spread
   // the chains over CUs (each message is a serial chain).
   const uint32_t wg = chain_workgroup(n);

@@ -92,15 +92,18 @@ def test_streaming_context_fields(bt, oracle):
 @contextlib.contextmanager
 def ragged_mode(bt, mode):
     """Pin ragged batches to the chain kernel ("chain": one workgroup per
-    message) or to the one-message-per-lane ragged kernel ("lanes")."""
+    message), the ragged latency kernel ("latr": loader / round waves per 64
+    messages) or the one-message-per-lane ragged kernel ("lanes")."""
     prev = bt.set_chain_batch(1 << 62 if mode == "chain" else 0)
+    prev_lat = bt.set_latency_batch(0 if mode == "lanes" else 1 << 62)
     try:
         yield
     finally:
         bt.set_chain_batch(prev)
+        bt.set_latency_batch(prev_lat)
 
 
-@pytest.fixture(params=["chain", "lanes"])
+@pytest.fixture(params=["chain", "latr", "lanes"])
 def rmode(bt, request):
     with ragged_mode(bt, request.param):
         yield request.param
@@ -900,3 +903,31 @@ def test_dropin_calls_from_many_threads(bt, oracle):
         a.update(ma[o:o + 4096])
         b.update(mb[o:o + 4096])
     assert a.final() == want[5] and b.final() == want[6]
+
+
+
+@pytest.mark.parametrize("n", [65, 600, 4099])
+def test_ragged_latency_kernel_mixed_lengths(bt, torch, oracle, n):
+    """k_sha1_lat_ragged: 64 messages per workgroup with unequal lengths (so
+    lanes finish at different blocks and latch their own state), every
+    residue mod 64 incl. messages shorter than one block (those lanes read a
+    static zero block), odd offsets; and the launch past one workgroup per CU
+    (three-slot form) at n = 4099.  Against the oracle."""
+    rng = random.Random(n)
+    lens = [rng.choice([0, 1, 55, 56, 63, 64, 65, 119, 120, 1000, rng.randrange(0, 40000)]) for _ in range(n)]
+    offs, pos = [], 0
+    for L in lens:
+        pos += rng.randrange(0, 16)
+        offs.append(pos)
+        pos += L
+    blob = bytes(oracle.fill_synthetic(pos + 64, n, 0x1A7))
+    d = to_dev(torch, blob)
+    ot = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    lt = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    out = torch.zeros(20 * n + 1, dtype=torch.uint8, device="cuda")
+    with ragged_mode(bt, "latr"):
+        bt.ragged_dev(d.data_ptr(), ot.data_ptr(), lt.data_ptr(), n, out.data_ptr() + 1)
+        torch.cuda.synchronize()
+    raw = bytes(out.cpu().numpy().tobytes())[1:]
+    for i in range(n):
+        assert raw[20 * i:20 * i + 20] == oracle.sha1(blob[offs[i]:offs[i] + lens[i]]), (n, i, lens[i])

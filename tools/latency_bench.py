@@ -96,7 +96,10 @@ def main():
 
     n = 4096
     lens = [int(x) for x in rng.integers(480 * 1024, 544 * 1024, n)]
-    for name, aligned in (("ragged_4096", True), ("ragged_4096_u", False)):
+    prev_lat = bt.set_latency_batch(2**64 - 1)
+    for name, aligned, lat in (("ragged_4096", True, 0), ("ragged_4096_u", False, 0),
+                               ("ragged_4096_latr", True, 2**64 - 1), ("ragged_4096_u_latr", False, 2**64 - 1)):
+        bt.set_latency_batch(lat)
         offs, pos = [], 0
         for ln in lens:
             pos += int(rng.integers(0, 16)) if not aligned else 0
@@ -113,9 +116,10 @@ def main():
             assert bytes(out[20 * i:20 * i + 20].cpu().numpy().tobytes()) == \
                 orc.sha1(host[offs[i]:offs[i] + lens[i]].tobytes()), (name, i)
         med = statistics.median(ts)
-        emit(name, ts, {"kernel": "k_sha1_ragged", "messages": n,
+        emit(name, ts, {"kernel": "k_sha1_lat_ragged" if lat else "k_sha1_ragged", "messages": n,
                         "GiB_per_s": round(sum(lens) / med / 2**30, 2)})
         del big
+    bt.set_latency_batch(prev_lat)
 
     # Streaming API at the peer's packet granule.
     ts = []

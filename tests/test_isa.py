@@ -187,3 +187,33 @@ def test_chain_kernel_round_wave_structure(asm):
     assert ops["ds_read_b128"] == 2 and ops["v_add_u32_dpp"] >= 70, ops
     assert ops["v_alignbit_b32"] == 160 and ops["v_bitop3_b32"] == 80, ops
 
+
+
+LAT_RAGGED = ["_ZN6btsha117k_sha1_lat_raggedILi2EE", "_ZN6btsha117k_sha1_lat_raggedILi3EE"]
+
+
+@pytest.mark.parametrize("prefix", LAT_RAGGED)
+def test_ragged_latency_loader_ring_keeps_loads_in_flight(asm, prefix):
+    """k_sha1_lat_ragged's loader wave reads each lane's own message through a
+    four-block register ring (messages of unequal length, so global loads, not
+    buffer loads): no wait right after a group of 16-byte loads may drain it
+    (vmcnt >= 4); the tail words are hoisted out of the per-block branch."""
+    _, text = asm
+    waits = _first_wait_after_each_load_group(text, _sym(text, prefix))
+    assert waits, "no 16-byte load groups found"
+    assert min(waits) >= 4, waits
+
+
+def test_ragged_latency_round_wave_structure(asm):
+    """Its round wave is k_sha1_lat's (405 VALU per block, 20 ds_read_b128
+    from one 80-word slot, one s_barrier) plus a handful of selects that latch
+    each lane's state at its own last block."""
+    import collections
+    _, text = asm
+    r_loops = [b for _, b in _loops(text, _sym(text, LAT_RAGGED[0])) if "ds_read_b128" in b]
+    assert len(r_loops) == 1, len(r_loops)
+    ops = collections.Counter(l.strip().split()[0] for l in r_loops[0].splitlines()
+                              if l.strip() and not l.strip().startswith((".", ";")))
+    valu = sum(v for k, v in ops.items() if k.startswith("v_"))
+    assert 405 <= valu <= 415, ops
+    assert ops["ds_read_b128"] == 20 and ops["s_barrier"] == 1, ops

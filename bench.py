@@ -25,6 +25,10 @@ rank 0 at N=1 additionally reports, after the timed region:
     use, at -O2 and at the reference Makefile's -O0 (SURVEY.md §8d);
   * host_path: config 5, the PCIe-inclusive host->digest rates of the
     pipelines that start in host memory (never `value`).
+Every rank (after the timed region, all together): `power`, the socket power
+of its GPU from the SMU energy accumulator while the timed step runs back to
+back for --power-s seconds, against the board's power cap (the bound that
+sets the hot kernel's clock).
 """
 import argparse
 import ctypes
@@ -129,6 +133,88 @@ class DeviceHasher:
         ratio = ((s[:, 2] - s[:, 0]) / (s[:, 3] - s[:, 1])).median().item()
         same = bool(torch.equal(scratch, self.dig))
         return ratio * self.bt.wallclock_khz() / 1000.0, same
+
+
+# ---------------------------------------------------------------------------
+# Board power while the hot kernel runs (the kernel is bounded by
+# the board power limit, not by HBM or VALU issue)
+# ---------------------------------------------------------------------------
+def _smi_handle(torch, dev):
+    """(amdsmi module, processor handle of HIP device `dev` matched by PCI
+    address) -- a box may expose one GPU to HIP and several to amdsmi."""
+    import amdsmi
+    amdsmi.amdsmi_init()
+    p = torch.cuda.get_device_properties(dev)
+    want = (int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
+    for h in amdsmi.amdsmi_get_processor_handles():
+        dom, bus, rest = amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")
+        if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
+            return amdsmi, h
+    return amdsmi, None
+
+
+def power_window(hasher, torch, dev, seconds):
+    """Run the timed step back to back for ~`seconds` after the timed region
+    and report the socket power from the SMU energy accumulator (delta energy /
+    delta wall time) and from current_socket_power samples (every 50 ms), with
+    the power cap, the per-XCD gfx clocks and the energy per GiB hashed."""
+    import statistics
+    smi, h = _smi_handle(torch, dev)
+    if h is None:
+        return {"error": "no amdsmi device with this GPU's PCI address"}
+    limit_w = smi.amdsmi_get_power_cap_info(h)["power_cap"] / 1e6  # reported in microwatts
+    per_launch_ms = hasher.kernel_ms() or 20.0
+    n = max(2, int(seconds * 1e3 / per_launch_ms))
+    samples, stop = [], threading.Event()
+
+    def sampler():
+        while not stop.is_set():
+            try:
+                m = smi.amdsmi_get_gpu_metrics_info(h)
+                clks = [c for c in m.get("current_gfxclks", []) if isinstance(c, (int, float))]
+                samples.append((float(m["current_socket_power"]), statistics.median(clks) if clks else None))
+            except Exception:  # noqa: BLE001 -- a missed sample is not an error
+                pass
+            stop.wait(0.05)
+
+    hasher.sync()
+    m0 = smi.amdsmi_get_gpu_metrics_info(h)
+    e0, t0 = smi.amdsmi_get_energy_count(h), time.perf_counter()
+    th = threading.Thread(target=sampler, daemon=True)
+    th.start()
+    for _ in range(n):
+        hasher.step(-1)
+    hasher.sync()
+    t1, e1 = time.perf_counter(), smi.amdsmi_get_energy_count(h)
+    m1 = smi.amdsmi_get_gpu_metrics_info(h)
+    stop.set()
+    th.join()
+    # Which limiter held the clock: the SMU's residency accumulators count the
+    # ticks (of accumulation_counter) each one was active over the window.
+    ticks = m1.get("accumulation_counter", 0) - m0.get("accumulation_counter", 0)
+    residency = {k[:-len("_residency_acc")]: round((m1[k] - m0[k]) / ticks, 4) for k in sorted(m1)
+                 if k.endswith("_residency_acc") and isinstance(m1[k], int) and isinstance(m0.get(k), int)
+                 and ticks > 0}
+    joules = (e1["energy_accumulator"] - e0["energy_accumulator"]) * e0["counter_resolution"] * 1e-6
+    watts = joules / (t1 - t0)
+    gibps = n * hasher.C * CHUNK / (t1 - t0) / 2**30
+    # the second half of the samples: after the power controller has settled
+    steady = samples[len(samples) // 2:]
+    sw = [w for w, _ in steady]
+    sc = [c for _, c in steady if c]
+    return {
+        "socket_W": round(watts, 1), "power_cap_W": round(limit_w, 1), "frac_of_cap": round(watts / limit_w, 4),
+        "sampled_socket_W_median": round(statistics.median(sw), 1) if sw else None,
+        "gfxclk_MHz_median": round(statistics.median(sc), 1) if sc else None,
+        "J_per_GiB": round(watts / gibps, 3), "GiB_per_s": round(gibps, 3),
+        "limiter_residency": residency,
+        "temperature_C": {k: m1.get(f"temperature_{k}") for k in ("hotspot", "mem")},
+        "launches": n, "window_s": round(t1 - t0, 3), "samples": len(samples),
+        "method": "after the timed region: the timed step launched back to back; socket_W = SMU energy "
+                  "accumulator delta / wall time (amdsmi_get_energy_count); samples = gpu_metrics "
+                  "current_socket_power / current_gfxclks every 50 ms, median of the second half; "
+                  "limiter_residency = fraction of SMU ticks each limiter (ppt = package power) was active",
+    }
 
 
 # ---------------------------------------------------------------------------
@@ -307,6 +393,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-clock", action="store_true")
+    ap.add_argument("--power-s", type=float, default=2.0,
+                    help="seconds of back-to-back steps after the timed region for the board-power reading (0 = off)")
     ap.add_argument("--backend", default="gloo",
                     help="process group for the control plane (barriers, timings, digest gather); "
                          "the hash path has no collective")
@@ -339,6 +427,30 @@ def main():
     first_chunk, _ = shard.weak_range(rank, C)
     hasher = DeviceHasher(bt, torch, C, pitch, first_chunk)
     res = shard.run_rank(hasher, args.steps, args.warmup, world, rank, group)
+    kernel = bt.kernel_name(C)
+
+    clock = None
+    if world == 1 and not args.no_clock and kernel == "k_sha1_fixed":
+        mhz, same = hasher.clock_mhz()
+        clock = {"in_kernel_mhz": round(mhz, 1), "probe_digests_identical": same,
+                 "method": "stamped build of the hot kernel (bt_sha1_clock_probe): median over waves of "
+                           "delta s_memtime / delta s_memrealtime x wall-clock rate, 3 launches after the "
+                           "timed region"}
+
+    # Every rank measures its own GPU's power (all ranks run the window together).
+    power = None
+    if args.power_s > 0:
+        try:
+            power = power_window(hasher, torch, dev, args.power_s)
+        except Exception as e:  # noqa: BLE001 -- the power evidence must never cost the bench line
+            power = {"error": f"{type(e).__name__}: {e}"}
+        keys = ("socket_W", "power_cap_W", "GiB_per_s", "gfxclk_MHz_median")
+        mine = [float(power.get(k) or -1.0) for k in keys]
+        allp = shard.gather_floats(mine, world, group)
+        if world > 1:
+            power = {"per_gpu": [dict(rank=r, **{k: (v if v >= 0 else None) for k, v in zip(keys, row)})
+                                 for r, row in enumerate(allp)],
+                     "method": power.get("method") if isinstance(power, dict) else None}
 
     line = None
     if rank == 0:
@@ -349,7 +461,6 @@ def main():
         bytes_per_launch = C * CHUNK
         achieved = bytes_per_launch / (kern_max * 1e-3) / 1e9
         valu_tops = C * (CHUNK // 64 + 1) * VALU_OPS_PER_BLOCK / (kern_max * 1e-3) / 1e12
-        kernel = bt.kernel_name(C)
 
         # Parity spot check of the timed output: global chunks 0..4095 are the
         # committed golden vectors (tests/golden/synth4096.txt, from sha.c).
@@ -358,14 +469,6 @@ def main():
         if os.path.exists(golden) and world * C >= 4096:
             rows = [l.split() for l in open(golden) if not l.startswith("#")]
             parity = all(all_dig[20 * int(i):20 * int(i) + 20].hex() == h for i, h in rows)
-
-        clock = None
-        if world == 1 and not args.no_clock and kernel == "k_sha1_fixed":
-            mhz, same = hasher.clock_mhz()
-            clock = {"in_kernel_mhz": round(mhz, 1), "probe_digests_identical": same,
-                     "method": "stamped build of the hot kernel (bt_sha1_clock_probe): median over waves of "
-                               "delta s_memtime / delta s_memrealtime x wall-clock rate, 3 launches after the "
-                               "timed region"}
 
         # PMC traffic, only when measured on this very build and layout.
         traffic, traffic_note = None, None
@@ -453,6 +556,7 @@ def main():
                               f"{VALU_FULL_RATE_PER_BLOCK} full-rate) on 1024 SIMDs at 2.4 GHz (peak) and at the "
                               "in-kernel clock (peak_at_measured_clock)"},
             "clock": clock,
+            "power": power,
             "per_gpu": [{"rank": r, "GiB_per_s": round(C * CHUNK * args.steps / w / 2**30, 3),
                          "kernel_ms": round(k, 4)} for r, (w, k) in enumerate(res["per_rank"])],
             "parity_first_4096_vs_golden": parity,

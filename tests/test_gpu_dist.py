@@ -51,3 +51,5 @@ def test_bench_ranks_split_and_gather_on_one_gpu(world):
     assert line["value"] > 0 and line["scaling"] == "weak"
     # N > 1: no CPU baseline / host-path legs (rank 0 at N = 1 only)
     assert line["cpu_baseline"] is None and line["host_path"] is None
+    # every rank read its own GPU's board power after the timed region
+    assert [p["rank"] for p in line["power"]["per_gpu"]] == list(range(world))

@@ -42,10 +42,10 @@ for step in "$@"; do
       # same process: the bench line (prof.log) and the rocprof kernel stats
       mkdir -p "$OUT/prof"
       run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench \
-        -- python3 "$ROOT/bench.py" --steps 20 --no-cpu-baseline --no-host-path --no-clock ;;
+        -- python3 "$ROOT/bench.py" --steps 20 --no-cpu-baseline --no-host-path --no-clock --power-s 0 ;;
     pmc)
       mkdir -p "$OUT/pmc"
-      PB="python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-path --no-clock"
+      PB="python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-path --no-clock --power-s 0"
       run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o fetch -- $PB
       run pmc_rdreq 600 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc" -o rdreq -- $PB
       run pmc_valu 600 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc" -o valu -- $PB

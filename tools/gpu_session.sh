@@ -140,6 +140,16 @@ for step in "$@"; do
       run power_stream2 300 "$ROOT/tools/ubench/streamread2" 400
       wait $sp ;;
     wgdist) run wgdist 120 "$ROOT/tools/ubench/wgdist" ;;
+    energy_ab)
+      # energy per GiB of each hot-kernel variant under the power cap, alternating
+      # rounds in one box session (bench.py's `power` object: SMU energy accumulator)
+      for rep in 1 2; do
+        for v in "3 1 0" "2 1 0" "4 1 0" "2 2 0" "10 1 0" "10 1 1"; do
+          set -- $v
+          run "energy_$1$2$3_$rep" 300 python3 bench.py --ring $1 --lines $2 --nt $3 --steps 20 \
+            --no-cpu-baseline --no-host-path --power-s 4
+        done
+      done ;;
     power)
       # sample board power and clocks while a ~30 s hot-kernel run is in flight
       ( for i in $(seq 1 12); do date +%T; timeout 10 amd-smi metric -g 0 -p -c 2>&1

@@ -27,6 +27,7 @@
 #include <thread>
 #include <vector>
 
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <cerrno>
@@ -115,11 +116,55 @@ struct PinBuf {
   T *as() const { return static_cast<T *>(p); }
 };
 
+void touch_parallel(uint8_t *p, uint64_t n);
+
+// Grow-only staging buffer of the host pipelines, read only by the DMA engine
+// (hipMemcpyAsync): anonymous memory on transparent huge pages, first-touched
+// by several threads, then page-locked with hipHostRegister.  Per GiB on
+// MI355X boxes (tools/ubench/pin_cost.hip): ~3 ms to register + the touch
+// (65 ms on one thread), against 222-251 ms for hipHostMalloc -- the pinning
+// was most of a make-chunks run on a 1 GiB file.  Same H2D rate (~57 GB/s).
+struct StageBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  void release() {
+    if (!p) return;
+    (void)hipHostUnregister(p);
+    munmap(p, cap);
+    p = nullptr;
+    cap = 0;
+  }
+  int ensure(size_t need) {
+    if (need <= cap) return 0;
+    release();
+    const size_t sz = (std::max<size_t>(need, 4096) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    void *q = mmap(nullptr, sz, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (q == MAP_FAILED) {
+      set_err("staging mmap of %zu bytes failed: %s", sz, strerror(errno));
+      return -1;
+    }
+    (void)madvise(q, sz, MADV_HUGEPAGE);  // a hint: 4 KiB pages still work
+    touch_parallel((uint8_t *)q, sz);
+    const hipError_t e = hipHostRegister(q, sz, hipHostRegisterPortable);
+    if (e != hipSuccess) {
+      munmap(q, sz);
+      set_err("hipHostRegister of the staging buffer failed: %s", hipGetErrorString(e));
+      return -1;
+    }
+    p = q;
+    cap = sz;
+    return 0;
+  }
+  template <class T>
+  T *as() const { return static_cast<T *>(p); }
+};
+
 // One double-buffered staging lane of the host pipelines.
 struct Lane {
   hipStream_t s = nullptr;
   hipEvent_t ev = nullptr;
-  PinBuf h_in, h_dig;  // h_dig: the kernel stores digests straight into it
+  StageBuf h_in;  // staged input pieces, DMA'd to d_in
+  PinBuf h_dig;   // the kernel stores digests straight into it
   DevBuf d_in;
   bool busy = false;
   uint64_t first = 0, count = 0;  // chunk range in flight
@@ -310,6 +355,12 @@ void parallel_pieces(uint64_t n, Body body) {
     th.emplace_back([&, i] { body((uint64_t)i * piece, std::min<uint64_t>(piece, n - (uint64_t)i * piece), i); });
   body(0, std::min<uint64_t>(piece, n), 0);
   for (auto &x : th) x.join();
+}
+
+void touch_parallel(uint8_t *p, uint64_t n) {
+  parallel_pieces(n, [&](uint64_t off, uint64_t len, int) {
+    for (uint64_t o = 0; o < len; o += 4096) p[off + o] = 0;
+  });
 }
 
 void parallel_copy(uint8_t *dst, const uint8_t *src, uint64_t n) {

@@ -1159,6 +1159,7 @@ void SHA1Final(SHA1Context *sc, uint8_t hash[SHA1_HASH_SIZE]) {
 struct VBatch {
   hipStream_t s = nullptr;
   hipEvent_t ev = nullptr;
+  StageBuf slots;  // the received chunks: written by the caller, read by the H2D copy
   uint8_t *h_in = nullptr, *h_exp = nullptr, *h_ok = nullptr, *h_dig = nullptr;
   uint8_t *d_in = nullptr;
   std::vector<uint64_t> tags;
@@ -1276,20 +1277,22 @@ bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32
   v->batch = batch;
   v->b.resize(std::max<uint32_t>(nstreams, 2));
   const size_t bytes = (size_t)batch * chunk_len;
+  t_err.clear();
   for (auto &b : v->b) {
     b.tags.resize(batch);
     b.state.assign(batch, 0);
     if (hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc((void **)&b.h_in, bytes, hipHostMallocDefault) != hipSuccess ||
+        b.slots.ensure(bytes) != 0 ||
         hipHostMalloc((void **)&b.h_exp, 20 * (size_t)batch, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&b.h_ok, batch, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&b.h_dig, 20 * (size_t)batch, hipHostMallocDefault) != hipSuccess ||
         hipMalloc((void **)&b.d_in, bytes) != hipSuccess) {
-      set_err("verifier: allocation failed");
+      if (t_err.empty()) set_err("verifier: allocation failed");
       bt_sha1_verifier_destroy(v);
       return nullptr;
     }
+    b.h_in = b.slots.as<uint8_t>();
   }
   return v;
 }
@@ -1302,7 +1305,7 @@ void bt_sha1_verifier_destroy(bt_sha1_verifier *v) {
     if (b.s) (void)hipStreamSynchronize(b.s);
     if (b.ev) (void)hipEventDestroy(b.ev);
     if (b.s) (void)hipStreamDestroy(b.s);
-    if (b.h_in) (void)hipHostFree(b.h_in);
+    b.slots.release();
     if (b.h_exp) (void)hipHostFree(b.h_exp);
     if (b.h_ok) (void)hipHostFree(b.h_ok);
     if (b.h_dig) (void)hipHostFree(b.h_dig);

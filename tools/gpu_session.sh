@@ -179,6 +179,10 @@ for step in "$@"; do
         run "dma_batch_$mb" 300 env BT_SHA1_DMA_BATCH_MB=$mb python3 tools/stream_bench.py 8
       done ;;
     filebench) run filebench 600 env BT_SHA1_TRACE=1 python3 tools/file_bench.py /dev/shm 1 1024 8192 32768 ;;
+    filethreads)
+      for t in 8 12 16 8 12 16; do
+        run "filethreads_$t" 300 env BT_SHA1_TRACE=1 BT_SHA1_COPY_THREADS=$t python3 tools/file_bench.py /dev/shm 8192 32768
+      done ;;
     vs_prof)
       python3 -c "import lzma; open('/tmp/C.tar','wb').write(lzma.decompress(open('tests/golden/C.tar.xz','rb').read()))"
       mkdir -p "$OUT/vs_prof"

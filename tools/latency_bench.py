@@ -8,6 +8,7 @@ make_chunks hashes its short last chunk alone (chunk.c:20-21).  This prints
 one JSON line per measurement (median of --reps):
 
   shahash_512k      shahash() of one 512 KiB host buffer, call to return
+  shahash_<n>B      shahash() of a short message: the fixed cost of a drop-in call
   ragged_1x512k     bt_sha1_ragged_dev over one device-resident 512 KiB message
   ragged_1x512k_u   the same message at an odd byte offset (unaligned loads)
   ragged_4096       4096 device-resident messages of 480-544 KiB at 16-byte
@@ -65,6 +66,17 @@ def main():
         ts.append(time.perf_counter() - t0)
     assert got == want
     emit("shahash_512k", ts)
+    # Fixed cost of one drop-in call: short messages (one launch of the chain
+    # kernel on pinned host memory + the spin on its completion word).
+    for ln in (0, 55, 1484, 16384):
+        m = msg[:ln]
+        assert bt.shahash(m) == orc.sha1(m)
+        ts = []
+        for _ in range(200):
+            t0 = time.perf_counter()
+            bt.shahash(m)
+            ts.append(time.perf_counter() - t0)
+        emit(f"shahash_{ln}B", ts)
 
     s = torch.cuda.Stream()
     torch.cuda.set_stream(s)

@@ -456,6 +456,26 @@ def test_verifier_async_batches(bt, oracle):
     v.close()
 
 
+def test_verifier_lifecycle_and_staging_growth(bt, oracle):
+    """Verifiers created and destroyed repeatedly (their chunk slots are
+    page-locked staging memory, registered and unregistered each time) and
+    host pipelines whose staging grows between calls keep exact results."""
+    img = c_tar_bytes()
+    chunks = [img[i * CHUNK:(i + 1) * CHUNK] for i in range(4)]
+    ref = [oracle.sha1(c) for c in chunks]
+    for batch, streams in ((1, 2), (7, 3), (4, 2), (16, 4), (2, 2)):
+        v = bt.Verifier(batch=batch, nstreams=streams)
+        for k in range(9):
+            v.slot_fill(chunks[k % 4], ref[k % 4] if k != 5 else bytes(20), tag=k)
+        got = v.drain()
+        v.close()
+        assert got == [(k, k != 5, ref[k % 4]) for k in range(9)], (batch, streams)
+    for mib in (1, 3, 70, 9):  # staging sized by the input, grow-only
+        data = (img * (mib // 2 + 1))[:mib * 1024 * 1024 + 777]
+        want = [oracle.sha1(data[o:o + CHUNK]) for o in range(0, len(data), CHUNK)]
+        assert bt.chunks_host(data) == want, mib
+
+
 def test_full_size_config3_properties(bt, torch, oracle):
     """BASELINE config 3 size (131072 x 512 KiB = 64 GiB in HBM): spot parity
     against the oracle on regenerated host data, determinism, distinctness."""

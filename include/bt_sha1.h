@@ -74,8 +74,9 @@ uint64_t bt_sha1_set_latency_batch(uint64_t max_chunks);
  * two per compute unit.  Returns the previous setting. */
 uint64_t bt_sha1_set_chain_batch(uint64_t max_messages);
 /* Name of the kernel a fixed-layout batch of n_chunks chunks runs on the
- * current device ("k_sha1_fixed", "k_sha1_lat" or "k_sha1_lds"); NULL without
- * a device. */
+ * current device ("k_sha1_chain" up to two chunks per CU, "k_sha1_lat" up to
+ * the latency batch, else "k_sha1_fixed" or, with variant 10, "k_sha1_lds");
+ * NULL without a device. */
 const char *bt_sha1_kernel_name(uint64_t n_chunks);
 /* Diagnostic (bench clock measurement): hashes the batch like
  * bt_sha1_chunks_dev through a separately compiled build of the hot kernel

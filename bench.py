@@ -158,10 +158,17 @@ def power_window(hasher, torch, dev, seconds):
     and report the socket power from the SMU energy accumulator (delta energy /
     delta wall time) and from current_socket_power samples (every 50 ms), with
     the power cap, the per-XCD gfx clocks and the energy per GiB hashed."""
-    import statistics
     smi, h = _smi_handle(torch, dev)
-    if h is None:
-        return {"error": "no amdsmi device with this GPU's PCI address"}
+    try:
+        if h is None:
+            return {"error": "no amdsmi device with this GPU's PCI address"}
+        return _power_window(smi, h, hasher, seconds)
+    finally:
+        smi.amdsmi_shut_down()
+
+
+def _power_window(smi, h, hasher, seconds):
+    import statistics
     limit_w = smi.amdsmi_get_power_cap_info(h)["power_cap"] / 1e6  # reported in microwatts
     per_launch_ms = hasher.kernel_ms() or 20.0
     n = max(2, int(seconds * 1e3 / per_launch_ms))

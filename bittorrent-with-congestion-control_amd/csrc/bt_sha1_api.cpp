@@ -144,6 +144,9 @@ struct StageBuf {
       return -1;
     }
     (void)madvise(q, sz, MADV_HUGEPAGE);  // a hint: 4 KiB pages still work
+    // Not inherited by fork(): a child (e.g. a subprocess about to exec) would
+    // otherwise get a copy of every page-locked page at fork time.
+    (void)madvise(q, sz, MADV_DONTFORK);
     touch_parallel((uint8_t *)q, sz);
     const hipError_t e = hipHostRegister(q, sz, hipHostRegisterPortable);
     if (e != hipSuccess) {

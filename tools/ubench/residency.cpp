@@ -6,7 +6,8 @@
 //   l2    pitch 16 B      all lanes of the grid walk the same ~2.5 MiB (L2-resident)
 // Same instruction stream, same grid in all three; only where the bytes come from
 // differs.  Prints ms per launch, the hashed-bytes rate and the wall-clock window
-// (to line up with power/clock samples).  Args: [chunks] [launches per mode] [rounds].
+// (to line up with power/clock samples).  Args: [chunks] [launches per mode] [rounds]
+// [mode: 0 hbm, 1 mall, 2 l2; default all].
 // Build: make ubench (links bittorrent-with-congestion-control_amd/libbtsha1.so).
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -21,6 +22,7 @@ int main(int argc, char **argv) {
   const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 0) : 131072, len = 512 * 1024;
   const int reps = argc > 2 ? atoi(argv[2]) : 10;  // ~20 ms per launch
   const int rounds = argc > 3 ? atoi(argv[3]) : 2;
+  const int only = argc > 4 ? atoi(argv[4]) : -1;  // 0 hbm, 1 mall, 2 l2; -1 all
   const uint64_t bytes = n * len;
   void *buf;
   uint8_t *dig;
@@ -34,7 +36,9 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e1));
   struct { const char *name; uint32_t pitch; } modes[] = {{"hbm", 512 * 1024}, {"mall", 1024}, {"l2", 16}};
   for (int round = 0; round < rounds; ++round)
-    for (auto &m : modes) {
+    for (int mi = 0; mi < 3; ++mi) {
+      if (only >= 0 && mi != only) continue;
+      auto &m = modes[mi];
       // footprint check: the last chunk must end inside the allocation
       if ((n - 1) * (uint64_t)m.pitch + len > bytes) { fprintf(stderr, "bad pitch\n"); return 1; }
       CK(btsha1_launch_fixed(buf, n, m.pitch, (uint32_t)len, dig, nullptr, nullptr, s, 310));  // warm

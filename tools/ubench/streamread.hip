@@ -57,6 +57,7 @@ __global__ __launch_bounds__(256) void k_coalesced(const unsigned char *buf, uns
 
 int main(int argc, char **argv) {
   const int launches = argc > 1 ? atoi(argv[1]) : 400;
+  const int only = argc > 2 ? atoi(argv[2]) : -1;  // one mode (0..3), -1 all
   const size_t n = 131072, chunk = 512 * 1024, bytes = n * chunk;
   unsigned char *buf;
   unsigned *out;
@@ -68,6 +69,7 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e1));
   const unsigned slabs = (unsigned)(bytes >> 20);
   for (int mode = 0; mode < 4; ++mode) {
+    if (only >= 0 && mode != only) continue;
     const char *names[] = {"perlane", "perlane_nt", "coalesced", "coalesced_nt"};
     auto launch = [&] {
       switch (mode) {

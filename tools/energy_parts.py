@@ -16,7 +16,8 @@ workload prints its own rate; energy per GiB = power / rate.
   stream    a read-only stream in the hot kernel's per-lane pattern
   coalesced a read-only stream, 8 lines per wave instruction
 
-One JSON line per case.  usage: energy_parts.py [seconds per case]
+One JSON line per case.  usage: energy_parts.py [seconds per case] [grouped]
+(`grouped`: only the read-only streams with G = 1, 2, 4, 8 lanes per line)
 """
 import json
 import os
@@ -101,6 +102,9 @@ def main():
         ("stream", [os.path.join(UB, "streamread"), str(int(secs * 1000 / 17)), "0"]),
         ("coalesced", [os.path.join(UB, "streamread"), str(int(secs * 1000 / 11)), "2"]),
     ]
+    if len(sys.argv) > 2 and sys.argv[2] == "grouped":  # read patterns only
+        cases = [cases[0]] + [(f"stream_g{g}", [os.path.join(UB, "streamread"), str(int(secs * 1000 / 15)), str(m)])
+                              for g, m in ((1, 0), (2, 4), (4, 5), (8, 6), (1, 0))]
     idle = None
     for name, cmd in cases:
         watts, clk, ppt, win_s, out = measure(h, cmd, secs)

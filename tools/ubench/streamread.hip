@@ -4,9 +4,10 @@
 //   perlane  the hot kernel's access pattern: one chunk per lane, a wave's 64
 //            lanes 512 KiB apart, 128 B per lane per batch of loads
 //   coalesced each wave reads a contiguous 1 MiB slab, 1 KiB per load instruction
+//   groupedG  perlane's ownership with G lanes per 128-byte line (G = 2, 4, 8)
 // each with default and non-temporal (nt) cache policy.  Run for ~10 s per mode so
 // board power can be sampled alongside (tools/gpu_session.sh power_stream).
-// Args: [launches per mode] (default 400).
+// Args: [launches per mode] (default 400) [mode 0..6, default all].
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -31,6 +32,28 @@ __global__ __launch_bounds__(256) void k_perlane(const unsigned char *buf, unsig
     u32x4 v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b128(r, lane * pitch + j * 16, pos, AUX);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc ^= v[j];
+  }
+  out[wave * 64 + lane] = acc.x ^ acc.y ^ acc.z ^ acc.w;
+}
+
+// The hot kernel's ownership (a wave owns 64 chunks, walks them 128 B at a
+// time), but G lanes share each line: instruction j reads chunk G*q + j%G of
+// lane group q, 16*G contiguous bytes at 16*G*(j/G) of the 128-byte step.
+// G = 1 is k_perlane; G = 8 reads whole lines (8 lines per instruction).
+template <int G>
+__global__ __launch_bounds__(256) void k_grouped(const unsigned char *buf, unsigned pitch, unsigned chunk, unsigned *out) {
+  const unsigned wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
+  const unsigned q = lane / G, r = lane % G;
+  const unsigned char *base = buf + (size_t)wave * 64 * pitch;
+  const __amdgpu_buffer_rsrc_t rs = rsrc(base, 64 * pitch);
+  u32x4 acc = {0, 0, 0, 0};
+  for (unsigned pos = 0; pos < chunk; pos += 128) {
+    u32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (G * q + j % G) * pitch + 16 * (G * (j / G) + r), pos, 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc ^= v[j];
   }
@@ -68,14 +91,17 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const unsigned slabs = (unsigned)(bytes >> 20);
-  for (int mode = 0; mode < 4; ++mode) {
+  for (int mode = 0; mode < 7; ++mode) {
     if (only >= 0 && mode != only) continue;
-    const char *names[] = {"perlane", "perlane_nt", "coalesced", "coalesced_nt"};
+    const char *names[] = {"perlane", "perlane_nt", "coalesced", "coalesced_nt", "grouped2", "grouped4", "grouped8"};
     auto launch = [&] {
       switch (mode) {
         case 0: hipLaunchKernelGGL(k_perlane<0>, dim3(n / 256), dim3(256), 0, 0, buf, chunk, chunk, out); break;
         case 1: hipLaunchKernelGGL(k_perlane<2>, dim3(n / 256), dim3(256), 0, 0, buf, chunk, chunk, out); break;
         case 2: hipLaunchKernelGGL(k_coalesced<0>, dim3(2048), dim3(256), 0, 0, buf, slabs, out); break;
+        case 4: hipLaunchKernelGGL(k_grouped<2>, dim3(n / 256), dim3(256), 0, 0, buf, chunk, chunk, out); break;
+        case 5: hipLaunchKernelGGL(k_grouped<4>, dim3(n / 256), dim3(256), 0, 0, buf, chunk, chunk, out); break;
+        case 6: hipLaunchKernelGGL(k_grouped<8>, dim3(n / 256), dim3(256), 0, 0, buf, chunk, chunk, out); break;
         default: hipLaunchKernelGGL(k_coalesced<2>, dim3(2048), dim3(256), 0, 0, buf, slabs, out); break;
       }
     };

@@ -1,7 +1,10 @@
 // sha1_kernels.hip -- gfx950 kernels of the SHA-1 chunk path + their launchers.
 //
-// Kernels (all one message per lane; SHA-1 is a serial Merkle-Damgard chain,
-// so parallelism is across chunks only -- SURVEY.md §7 "Serial chain"):
+// SHA-1 is a serial Merkle-Damgard chain (SURVEY.md §7 "Serial chain"), so
+// parallelism is across messages only.  The throughput kernels give each lane
+// one message; the latency kernels split one chain's work between a loader /
+// schedule wave S and a round wave R that meet in LDS.  Which kernel a batch
+// runs follows from its size and the device's CU count.
 //   k_sha1_fixed    the hot path: n equal-length chunks at a fixed pitch in HBM
 //                   (make_chunks' 512 KiB chunks, chunk.c:20-21; received-chunk
 //                   verify, util.c:311-313, when VERIFY).  Each lane streams its
@@ -17,12 +20,17 @@
 //                   MI355X: small verify batches): a loader/schedule wave and a round
 //                   wave per 64 chunks meet in LDS, cutting a lone chain's
 //                   instruction count from 597 to ~426 per block.
+//   k_sha1_chain    ONE message per two-wave workgroup (<= 2 chunks per CU;
+//                   shahash, SHA1Update/SHA1Final midstates): S prepares 64 of
+//                   the message's blocks at a time, R runs them back to back.
+//   k_sha1_lat_ragged  k_sha1_lat's split for 64 messages of any lengths and
+//                   alignment (ragged batches of 2 .. 128 per CU).
 //   k_sha1_ragged   arbitrary (offset, length) messages and layouts the
 //                   fixed kernels do not take (pitch not a 16-byte multiple,
-//                   offsets past 4 GiB per wave).
-//   k_sha1_midstate chaining-state update over whole blocks: the GPU side of
-//                   the streaming SHA1Update/SHA1Final API (sha.c:453-558).
+//                   offsets past 4 GiB per wave), one message per lane.
 //   k_fill_synthetic  frozen counter-based generator (bench/test data in HBM).
+//   k_lookup_build / k_lookup_query  digest -> first index table in HBM
+//                   (get_chunk_id / find_chunk, util.c:3-39).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -996,14 +1004,6 @@ __global__ __launch_bounds__(kBlock) void k_sha1_ragged(const uint8_t *__restric
   }
 }
 
-// state[5] (host-order words, as SHA1Context.hash) advanced over nblocks blocks.
-__global__ void k_sha1_midstate(uint32_t *__restrict__ state, const uint8_t *__restrict__ p, uint64_t nblocks) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  State st{state[0], state[1], state[2], state[3], state[4]};
-  absorb_blocks(st, p, nblocks);
-  state[0] = st.h0; state[1] = st.h1; state[2] = st.h2; state[3] = st.h3; state[4] = st.h4;
-}
-
 // ---------------------------------------------------------------------------
 // Frozen synthetic generator: word g of the stream = splitmix64(seed + g),
 // stored little-endian (mirrored by oracle/sha1_oracle.c:or_fill_synthetic).
@@ -1286,11 +1286,6 @@ hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const
   const uint64_t grid = (n + wg - 1) / wg;
   hipLaunchKernelGGL(k_sha1_ragged, dim3((uint32_t)grid), dim3(wg), 0, s, (const uint8_t *)d_base, d_off,
                      d_len, pitch, fixed_len, n, d_dig);
-  return hipGetLastError();
-}
-
-hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_t nblocks, hipStream_t s) {
-  hipLaunchKernelGGL(k_sha1_midstate, dim3(1), dim3(64), 0, s, d_state, (const uint8_t *)d_data, nblocks);
   return hipGetLastError();
 }
 

@@ -43,8 +43,6 @@ bool btsha1_fixed_variant_ok(int code);
 // per-lane ragged kernel.
 hipError_t btsha1_launch_ragged(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, uint64_t pitch,
                                 uint32_t fixed_len, uint64_t n, uint8_t *d_dig, hipStream_t s);
-// d_state[5] advanced over nblocks whole 64-byte blocks at d_data.
-hipError_t btsha1_launch_midstate(uint32_t *d_state, const void *d_data, uint64_t nblocks, hipStream_t s);
 // Chain kernel (one message per two-wave workgroup; lowest single-chain
 // latency).  state / data may be device or pinned host memory.
 // done != NULL: after the results, *done = seq is stored with a system-scope

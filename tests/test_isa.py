@@ -99,7 +99,7 @@ def _first_wait_after_each_load_group(text, sym, load="global_load_dwordx4"):
     return out
 
 
-@pytest.mark.parametrize("sym", ["_ZN6btsha113k_sha1_raggedEPKhPKmPKjmjmPh", "_ZN6btsha115k_sha1_midstateEPjPKhm"])
+@pytest.mark.parametrize("sym", ["_ZN6btsha113k_sha1_raggedEPKhPKmPKjmjmPh"])
 def test_ragged_ring_keeps_loads_in_flight(asm, sym):
     """The generic kernels' prefetch ring (absorb_ring) must not wait for the
     block it just asked for: the first wait after each group of four 16-byte

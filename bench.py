@@ -115,6 +115,13 @@ class DeviceHasher:
     def kernel_ms(self):
         return sum(a.elapsed_time(b) for a, b in self.ev) / len(self.ev) if self.ev else None
 
+    def kernel_ms_median(self):
+        """SURVEY.md §8d's config-3 statistic (median of the timed launches)."""
+        if not self.ev:
+            return None
+        t = sorted(a.elapsed_time(b) for a, b in self.ev)
+        return (t[(len(t) - 1) // 2] + t[len(t) // 2]) / 2
+
     def digests(self):
         return self.dig.cpu().numpy().tobytes()
 
@@ -551,6 +558,7 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": kernel, "kernel_ms": round(kern_max, 4),
+                "kernel_ms_median_rank0": round(hasher.kernel_ms_median(), 4),
                 "algorithmic_bytes_per_launch": bytes_per_launch, "traffic_source": traffic_note,
             },
             "valu_roofline": None if kernel != "k_sha1_fixed" else {

@@ -13,7 +13,7 @@ BIN      := $(PKG)/bin
 
 REF      ?= /root/reference
 
-all: lib tools oracle dropin
+all: lib tools oracle dropin asan
 
 lib: $(LIB)
 

@@ -7,7 +7,10 @@ ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC)
 # Source id of the kernels (bt_sha1_source_id): profiles record it, bench.py
 # checks it before reusing PMC traffic measured on another build.
-SRC_ID   := $(shell cat $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h | sha256sum | cut -c1-16)
+# Comments are stripped first (gcc -fpreprocessed: no macro expansion, no
+# includes), so a comment-only edit keeps the id and the profiles tied to it.
+SRC_ID   := $(shell for f in $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h; do \
+              gcc -fpreprocessed -dD -E -P -x c++ $$f 2>/dev/null; done | sha256sum | cut -c1-16)
 LIB      := $(PKG)/libbtsha1.so
 BIN      := $(PKG)/bin
 

@@ -50,7 +50,8 @@ const char *bt_sha1_last_error(void);
  * source id). */
 const char *bt_sha1_build_info(void);
 /* Id of the kernel sources this library was compiled from (first 16 hex
- * digits of the SHA-256 of sha1_kernels.hip + sha1_device.h): ties profiles
+ * digits of the SHA-256 of sha1_kernels.hip + sha1_device.h, comments
+ * stripped, so comment edits keep it): ties profiles
  * (PMC traffic, rocprof summaries) to the build that produced them. */
 const char *bt_sha1_source_id(void);
 /* Hot-kernel register-ring depth in 128-byte lines (2, 3 or 4; default 3).

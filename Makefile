@@ -9,14 +9,20 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC
 # checks it before reusing PMC traffic measured on another build.
 # Comments are stripped first (gcc -fpreprocessed: no macro expansion, no
 # includes), so a comment-only edit keeps the id and the profiles tied to it.
-SRC_ID   := $(shell for f in $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h; do \
-              gcc -fpreprocessed -dD -E -P -x c++ $$f 2>/dev/null; done | sha256sum | cut -c1-16)
+# Any gcc failure or an empty result falls back to hashing the raw files
+# (prefix "raw-"), so a broken strip can never alias every build to one id.
+KSRC     := $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h
+SRC_ID   := $(shell out=$$(for f in $(KSRC); do gcc -fpreprocessed -dD -E -P -x c++ $$f 2>/dev/null || exit 1; done) \
+              && [ -n "$$out" ] && printf '%s\n' "$$out" | sha256sum | cut -c1-16)
+ifeq ($(strip $(SRC_ID)),)
+SRC_ID   := raw-$(shell cat $(KSRC) | sha256sum | cut -c1-12)
+endif
 LIB      := $(PKG)/libbtsha1.so
 BIN      := $(PKG)/bin
 
 REF      ?= /root/reference
 
-all: lib tools oracle dropin asan
+all: lib tools oracle dropin asan dbgbar
 
 lib: $(LIB)
 
@@ -78,17 +84,33 @@ endif
 # Host-side AddressSanitizer/UBSan build of the library + native stress driver
 # (GPU code is not instrumented; GPU ASan is not available on this pool).
 ASANDIR  := build_variants/asan
+# The ASan runtime is linked shared (-shared-libasan): same image on the GPU
+# box, and the static runtime would ship ~3 MB per lease.
+ASANRT   := $(dir $(shell /opt/rocm/llvm/bin/clang -print-file-name=libclang_rt.asan-x86_64.so 2>/dev/null))
 ASANFLAGS := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer
 asan: $(ASANDIR)/host_stress
 
 $(ASANDIR)/libbtsha1.so: $(CSRC)/bt_sha1_api.cpp $(CSRC)/bt_chunks.cpp $(PKG)/build/sha1_kernels.o include/bt_sha1.h
 	@mkdir -p $(ASANDIR)
-	$(HIPCC) $(HIPFLAGS) -g $(ASANFLAGS) -c $(CSRC)/bt_sha1_api.cpp -o $(ASANDIR)/bt_sha1_api.o
-	$(HIPCC) $(HIPFLAGS) -g $(ASANFLAGS) -c $(CSRC)/bt_chunks.cpp -o $(ASANDIR)/bt_chunks.o
+	$(HIPCC) $(HIPFLAGS) -gline-tables-only $(ASANFLAGS) -c $(CSRC)/bt_sha1_api.cpp -o $(ASANDIR)/bt_sha1_api.o
+	$(HIPCC) $(HIPFLAGS) -gline-tables-only $(ASANFLAGS) -c $(CSRC)/bt_chunks.cpp -o $(ASANDIR)/bt_chunks.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PKG)/build/sha1_kernels.o $(ASANDIR)/bt_sha1_api.o $(ASANDIR)/bt_chunks.o
 
 $(ASANDIR)/host_stress: tests/native/host_stress.c $(ASANDIR)/libbtsha1.so
-	/opt/rocm/llvm/bin/clang -g -O1 -fsanitize=address,undefined -fno-omit-frame-pointer -Iinclude -o $@ $< -L$(ASANDIR) -lbtsha1 -Wl,-rpath,'$$ORIGIN'
+	/opt/rocm/llvm/bin/clang -gline-tables-only -O1 -fsanitize=address,undefined -shared-libasan -fno-omit-frame-pointer -Iinclude -o $@ $< \
+	    -L$(ASANDIR) -lbtsha1 -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(ASANRT)
+
+# Barrier-accounting build: the latency / chain / ragged-latency kernels count
+# the s_barriers each wave executes and check them against the invariant they
+# rely on (sha1_kernels.hip, "Barrier accounting"); bt_sha1_debug_barrier_stats
+# reads the tallies.  Same API objects, only the kernel object differs.  Run by
+# tests/test_gpu_barriers.py in a child process (BT_SHA1_LIB points at it).
+DBGDIR   := build_variants/dbgbar
+dbgbar: $(DBGDIR)/libbtsha1.so
+$(DBGDIR)/libbtsha1.so: $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h $(CSRC)/sha1_launch.h $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o
+	@mkdir -p $(DBGDIR)
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_DEBUG_BARRIERS -c $< -o $(DBGDIR)/sha1_kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(DBGDIR)/sha1_kernels.o $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o -Wl,-soname,libbtsha1.so
 
 # Scheduler-strategy builds of the library (experiment in profiles/r01/experiments.md;
 # tools/gpu_session.sh libvariants benches each).  Not part of the product.
@@ -117,4 +139,4 @@ clean:
 	rm -rf $(PKG)/build $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib tools oracle dropin asan ubench sched_variants clean
+.PHONY: all lib tools oracle dropin asan dbgbar ubench sched_variants clean

@@ -68,6 +68,7 @@ _sig("bt_sha1_set_chain_batch", _u64, _u64)
 _sig("bt_sha1_kernel_name", ctypes.c_char_p, _u64)
 _sig("bt_sha1_clock_probe", ctypes.c_int, _vp, _u64, _u64, _u64, _vp, _vp, _vp)
 _sig("bt_sha1_wallclock_khz", _i64)
+_sig("bt_sha1_debug_barrier_stats", ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int)
 _sig("bt_sha1_chunks_file", _i64, _vp, _u64, _vp, _u64)
 _sig("bt_sha1_verifier_create", _vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32)
 _sig("bt_sha1_verifier_destroy", None, _vp)
@@ -157,6 +158,15 @@ def clock_probe(d_in, n, chunk_len, pitch, d_digests, d_stamps, stream=None):
 
 def wallclock_khz():
     return _check(lib.bt_sha1_wallclock_khz(), "bt_sha1_wallclock_khz")
+
+
+def debug_barrier_stats(reset=False):
+    """(waves checked, barriers executed, invariant misses) of the barrier-
+    accounting build (make dbgbar, loaded with BT_SHA1_LIB); raises on the
+    production library, which counts nothing."""
+    out = (ctypes.c_uint64 * 3)()
+    _check(lib.bt_sha1_debug_barrier_stats(out, 1 if reset else 0), "bt_sha1_debug_barrier_stats")
+    return tuple(int(x) for x in out)
 
 
 # ---- device-resident (addresses are ints) ------------------------------------

@@ -96,6 +96,11 @@ struct DevBuf {
     cap = sz;
     return 0;
   }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
   template <class T>
   T *as() const { return static_cast<T *>(p); }
 };
@@ -111,6 +116,11 @@ struct PinBuf {
     BT_CK(hipHostMalloc(&p, sz, hipHostMallocDefault));
     cap = sz;
     return 0;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
   }
   template <class T>
   T *as() const { return static_cast<T *>(p); }
@@ -184,9 +194,6 @@ struct DevCtx {
 
 std::mutex g_ctx_mu;
 std::vector<std::unique_ptr<DevCtx>> g_ctx;
-// Extra worker contexts (own streams and staging) for a device listed more
-// than once in bt_sha1_chunks_host_devices; index k-1 = its k-th repeat.
-std::vector<std::vector<std::unique_ptr<DevCtx>>> g_extra;
 
 int device_count() {
   int n = 0;
@@ -219,20 +226,28 @@ DevCtx *ctx_for(int dev) {
   return g_ctx[dev].get();
 }
 
-// Context for the k-th use of `dev` inside one multi-device call (k = 0 is the
-// device's own context, shared with every other entry point).
-DevCtx *worker_ctx(int dev, int k) {
-  DevCtx *base = ctx_for(dev);
-  if (!base || k == 0) return base;
-  std::lock_guard<std::mutex> g(g_ctx_mu);
-  if ((int)g_extra.size() <= dev) g_extra.resize(dev + 1);
-  auto &v = g_extra[dev];
-  while ((int)v.size() < k) {
-    auto c = std::make_unique<DevCtx>();
-    c->dev = dev;
-    v.push_back(std::move(c));
+// Everything a context holds: its streams (drained first), staging lanes and
+// drop-in buffers.  Used for the per-call worker contexts of repeated device
+// ids in bt_sha1_chunks_host_devices, which must not outlive the call.
+void release_ctx(DevCtx *c) {
+  if (!c) return;
+  KeepDevice keep_dev;
+  if (hipSetDevice(c->dev) != hipSuccess) return;
+  for (auto &l : c->lane) {
+    if (l.s) {
+      (void)hipStreamSynchronize(l.s);
+      (void)hipStreamDestroy(l.s);
+    }
+    if (l.ev) (void)hipEventDestroy(l.ev);
+    l.s = nullptr;
+    l.ev = nullptr;
+    l.h_in.release();
+    l.h_dig.release();
+    l.d_in.release();
   }
-  return v[k - 1].get();
+  c->s = nullptr;
+  c->h_msg.release();
+  c->h_state.release();
 }
 
 // Streams are created on first use and kept few: HIP multiplexes streams onto
@@ -331,6 +346,10 @@ bool is_pinned(const void *p) {
   }
   return a.type == hipMemoryTypeHost;
 }
+
+// Workers of one bt_sha1_chunks_host_devices call (each a host thread with two
+// staging lanes of up to 1 GiB pinned + 1 GiB HBM while the call runs).
+constexpr int kMaxWorkers = 64;
 
 // Host staging threads for the pipelines' CPU side (memcpy into pinned memory,
 // file reads): one core moves ~8 GB/s, PCIe takes ~53.  BT_SHA1_COPY_THREADS
@@ -524,6 +543,12 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   if (join_pre()) return -1;  // input shorter than the size hint
   // Older lane first so digests arrive in order.
   if (drain(c->lane[k & 1]) || drain(c->lane[(k + 1) & 1])) return -1;
+  // Direct-DMA batches (up to BT_SHA1_DMA_BATCH_MB, 4 GiB by default) are not
+  // kept past the call: the lanes keep at most a staged batch (1 GiB) of HBM
+  // each, so a process that shares the GPU does not lose 8 GiB for good.
+  if (!staged)
+    for (auto &l : c->lane)
+      if (l.d_in.cap > batch_bytes_for(chunk_len, UINT64_MAX, true)) l.d_in.release();
   if (trace_on())
     fprintf(stderr, "libbtsha1 pipeline dev %d: %llu chunks, batch %llu B, %s: total %.4f s = alloc %.4f + fill %.4f "
                     "+ wait %.4f + other\n",
@@ -532,10 +557,12 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   return (int64_t)next;
 }
 
+// own: a worker context of this call (repeated device ids); NULL = the
+// device's shared context.
 int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t chunk_len, uint8_t *h_dig,
-                       int worker = 0) {
+                       DevCtx *own = nullptr) {
   KeepDevice keep_dev;
-  DevCtx *c = worker_ctx(dev, worker);
+  DevCtx *c = own ? own : ctx_for(dev);
   if (!c) return -1;
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(dev) != hipSuccess) {
@@ -799,6 +826,20 @@ int64_t bt_sha1_wallclock_khz(void) {
   return khz;
 }
 
+int bt_sha1_debug_barrier_stats(uint64_t out[3], int reset) {
+  if (!out) {
+    set_err("null pointer");
+    return -1;
+  }
+  const hipError_t e = btsha1_debug_barrier_stats(out, reset);
+  if (e == hipErrorNotSupported) {
+    set_err("barrier tallies exist only in the -DBT_SHA1_DEBUG_BARRIERS build (make dbgbar)");
+    return -1;
+  }
+  BT_CK(e);
+  return 0;
+}
+
 int bt_sha1_set_variant(int nbuf, int lines, int nt) {
   const int code = nbuf * 100 + lines * 10 + (nt ? 1 : 0);
   if (!btsha1_fixed_variant_ok(code)) {
@@ -938,6 +979,10 @@ int64_t bt_sha1_chunks_host_devices(const void *h_in, uint64_t total_len, uint64
     set_err("empty device list");
     return -1;
   }
+  if (nworkers > kMaxWorkers) {
+    set_err("%d workers: at most %d (one host thread and two staging lanes each)", nworkers, kMaxWorkers);
+    return -1;
+  }
   if (total_len == 0) return 0;
   if (!h_in || !h_digests) {
     set_err("null pointer");
@@ -958,12 +1003,25 @@ int64_t bt_sha1_chunks_host_devices(const void *h_in, uint64_t total_len, uint64
   // [g*n/G, (g+1)*n/G) -- possibly empty when G > n; only the globally last
   // chunk can be short.  One host thread per worker; a device listed k times
   // gets k independent contexts (streams + staging lanes), so the split,
-  // staging and ordered gather run exactly as on k distinct GPUs.
+  // staging and ordered gather run exactly as on k distinct GPUs.  The first
+  // use of a device takes its shared context; the repeats get contexts of
+  // their own that are released (buffers, streams) before the call returns.
   std::vector<int64_t> rc(nworkers, 0);
   std::vector<std::string> errs(nworkers);
-  std::vector<int> repeat(nworkers, 0);
+  std::vector<std::unique_ptr<DevCtx>> own(nworkers);
   for (int g = 0; g < nworkers; ++g)
-    for (int h = 0; h < g; ++h) repeat[g] += devs[h] == devs[g];
+    for (int h = 0; h < g; ++h)
+      if (devs[h] == devs[g]) {
+        own[g] = std::make_unique<DevCtx>();
+        own[g]->dev = devs[g];
+        break;
+      }
+  struct ReleaseAtExit {
+    std::vector<std::unique_ptr<DevCtx>> &v;
+    ~ReleaseAtExit() {
+      for (auto &c : v) release_ctx(c.get());
+    }
+  } release_at_exit{own};
   std::vector<std::thread> th;
   for (int g = 0; g < nworkers; ++g) {
     th.emplace_back([&, g] {
@@ -971,7 +1029,7 @@ int64_t bt_sha1_chunks_host_devices(const void *h_in, uint64_t total_len, uint64
       if (lo == hi) return;
       const uint64_t off = lo * chunk_len;
       const uint64_t bytes = std::min<uint64_t>(hi * chunk_len, total_len) - off;
-      rc[g] = chunks_host_on(devs[g], (const uint8_t *)h_in + off, bytes, chunk_len, h_digests + 20 * lo, repeat[g]);
+      rc[g] = chunks_host_on(devs[g], (const uint8_t *)h_in + off, bytes, chunk_len, h_digests + 20 * lo, own[g].get());
       if (rc[g] >= 0 && (uint64_t)rc[g] != hi - lo) {
         rc[g] = -1;
         t_err = "short digest count";

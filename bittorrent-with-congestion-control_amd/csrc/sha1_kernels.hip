@@ -395,18 +395,28 @@ __device__ __forceinline__ void produce_wk(uint32_t (&w)[16], u32x4 *slot, uint3
 // workgroup barrier is met from different call sites; s_barrier counts WAVES,
 // and the kernel is correct only while both waves execute exactly the same
 // number of barriers: nb_total + SLOTS - 1 each (S: one per produced block +
-// SLOTS - 1 final; R: SLOTS - 1 before its loop + one per consumed block).  Any edit that
-// changes one side's block count deadlocks the workgroup silently.  Build
-// with -DBT_SHA1_DEBUG_BARRIERS to count them per wave and trap on a mismatch.
+// SLOTS - 1 final; R: SLOTS - 1 before its loop + one per consumed block).  Any
+// edit that changes one side's block count pairs the waves' barriers wrongly
+// (S then overwrites a slot R is still reading) or leaves a wave waiting.
+// Build with -DBT_SHA1_DEBUG_BARRIERS (`make dbgbar`) to count them per wave:
+// every wave adds one check, its barrier count and, on a mismatch, one miss
+// to g_bar_stats (vector atomics, lane 0), which bt_sha1_debug_barrier_stats
+// reads back -- tests/test_gpu_barriers.py asserts zero misses AND the exact
+// total the invariant predicts for each launch shape.
 #ifdef BT_SHA1_DEBUG_BARRIERS
+__device__ unsigned long long g_bar_stats[3];  // {waves checked, barriers counted, mismatches}
 #define BT_LAT_BARRIER(cnt) \
   do {                      \
     ++(cnt);                \
     __syncthreads();        \
   } while (0)
-#define BT_LAT_CHECK(cnt, want) \
-  do {                          \
-    if ((cnt) != (want)) __builtin_trap(); \
+#define BT_LAT_CHECK(cnt, want)                                              \
+  do {                                                                       \
+    if ((threadIdx.x & 63u) == 0) {                                          \
+      atomicAdd(&g_bar_stats[0], 1ull);                                      \
+      atomicAdd(&g_bar_stats[1], (unsigned long long)(cnt));                 \
+      if ((uint64_t)(cnt) != (uint64_t)(want)) atomicAdd(&g_bar_stats[2], 1ull); \
+    }                                                                        \
   } while (0)
 #else
 #define BT_LAT_BARRIER(cnt) __syncthreads()
@@ -1328,6 +1338,25 @@ hipError_t btsha1_launch_lookup(const uint8_t *d_table, uint64_t n, const uint8_
   if (m) hipLaunchKernelGGL(k_lookup_query, dim3((uint32_t)((m + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, d_table,
                             d_slots, cap - 1, d_queries, m, d_index);
   return hipGetLastError();
+}
+
+// Barrier tallies of the -DBT_SHA1_DEBUG_BARRIERS build (g_bar_stats): copy
+// them out (and optionally zero them) after a device synchronisation.
+// hipErrorNotSupported in the production build, which counts nothing.
+hipError_t btsha1_debug_barrier_stats(uint64_t out[3], int reset) {
+#ifdef BT_SHA1_DEBUG_BARRIERS
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bar_stats), 3 * sizeof(uint64_t));
+  if (e == hipSuccess && reset) {
+    const uint64_t zero[3] = {0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_bar_stats), zero, sizeof zero);
+  }
+  return e;
+#else
+  (void)out;
+  (void)reset;
+  return hipErrorNotSupported;
+#endif
 }
 
 hipError_t btsha1_launch_fill(void *d_buf, uint64_t nbytes, uint64_t first_word, uint64_t seed, hipStream_t s) {

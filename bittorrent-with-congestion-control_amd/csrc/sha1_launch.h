@@ -66,3 +66,7 @@ hipError_t btsha1_launch_fill(void *d_buf, uint64_t nbytes, uint64_t first_word,
 // d_slots: cap (power of two, > n) u32 scratch.
 hipError_t btsha1_launch_lookup(const uint8_t *d_table, uint64_t n, const uint8_t *d_queries, uint64_t m,
                                 uint32_t *d_slots, uint32_t cap, int64_t *d_index, hipStream_t s);
+// Barrier tallies {waves checked, barriers counted, mismatches} of a
+// -DBT_SHA1_DEBUG_BARRIERS build (synchronises the device first; reset != 0
+// zeroes them); hipErrorNotSupported in the production build.
+hipError_t btsha1_debug_barrier_stats(uint64_t out[3], int reset);

@@ -48,9 +48,37 @@ static void count(const bt_sha1_verdict *out, int m, long *good, long *bad) {
   }
 }
 
+/* -z: which chunk each pinned slot holds (seq = order of the fill in round 0). */
+struct resident {
+  const uint8_t *slot;
+  long seq;
+  int k;
+};
+
+/* by slot address, then by fill order */
 static int cmp_resident(const void *a, const void *b) {
-  const uint8_t *x = *(const uint8_t *const *)a, *y = *(const uint8_t *const *)b;
+  const struct resident *x = (const struct resident *)a, *y = (const struct resident *)b;
+  if (x->slot != y->slot) return x->slot < y->slot ? -1 : 1;
+  return x->seq < y->seq ? -1 : x->seq > y->seq;
+}
+
+/* by slot address alone (lookups after index_resident) */
+static int cmp_slot(const void *a, const void *b) {
+  const uint8_t *x = ((const struct resident *)a)->slot, *y = ((const struct resident *)b)->slot;
   return x < y ? -1 : x > y;
+}
+
+/* Sort the round-0 fills and keep one entry per slot: the LAST fill of a slot
+ * is the chunk resident in it (a poll may recycle a batch inside round 0, so a
+ * slot can be handed out twice).  Returns the new count. */
+static long index_resident(struct resident *res, long nres) {
+  qsort(res, nres, sizeof *res, cmp_resident);
+  long m = 0;
+  for (long i = 0; i < nres; i++) {
+    if (m && res[m - 1].slot == res[i].slot) m--; /* a later fill of the same slot wins */
+    res[m++] = res[i];
+  }
+  return m;
 }
 
 static double now(void) {
@@ -134,7 +162,7 @@ int main(int argc, char **argv) {
    * ring order, but after a drain it resumes at whichever batch is next, so
    * the i-th slot of a later round is not the i-th slot of round 0: every
    * commit is paired with the chunk actually resident in the slot it got. */
-  struct resident { const uint8_t *slot; int k; } *res = NULL;
+  struct resident *res = NULL;
   long nres = 0;
   if (zcopy) res = malloc(sizeof *res * ring);
   bt_sha1_verdict out[256];
@@ -148,7 +176,7 @@ int main(int argc, char **argv) {
       t0 = now();
       timed = 0;
     }
-    if (zcopy && r == 1) qsort(res, nres, sizeof *res, cmp_resident);
+    if (zcopy && r == 1) nres = index_resident(res, nres);
     for (long i = 0; i < per_round; i++) {
       int k = (int)(i % n);
       const uint64_t off = (uint64_t)ids[k] * BT_CHUNK_SIZE;
@@ -159,9 +187,10 @@ int main(int argc, char **argv) {
       }
       if (zcopy && r == 0) {
         res[nres].slot = slot;
+        res[nres].seq = nres;
         res[nres++].k = k;
       } else if (zcopy) {
-        struct resident key = {slot, 0}, *hit = bsearch(&key, res, nres, sizeof *res, cmp_resident);
+        struct resident key = {slot, 0, 0}, *hit = bsearch(&key, res, nres, sizeof *res, cmp_slot);
         if (!hit) {
           fprintf(stderr, "verify-stream: slot %p was never filled\n", (void *)slot);
           return 255;

@@ -90,6 +90,15 @@ int bt_sha1_clock_probe(const void *d_in, uint64_t n, uint64_t chunk_len, uint64
                         uint64_t *d_stamps, void *stream);
 /* Rate of s_memrealtime on the current device in kHz (100000 on MI355X). */
 int64_t bt_sha1_wallclock_khz(void);
+/* Diagnostic (barrier-accounting build, `make dbgbar`): the latency, chain
+ * and ragged-latency kernels meet s_barrier from different call sites in
+ * their two waves and are correct only while both waves execute the same
+ * count.  That build tallies, over every such wave since the last reset,
+ * out[0] = waves checked, out[1] = barriers executed, out[2] = waves whose
+ * count broke the invariant.  Synchronises the current device first; reset
+ * != 0 zeroes the tallies after reading.  Returns -1 in the production
+ * library, which counts nothing. */
+int bt_sha1_debug_barrier_stats(uint64_t out[3], int reset);
 
 /* ---- device-resident batches (the hot path) ---------------------------- */
 /* n chunks of chunk_len bytes, chunk i at d_in + i*pitch (pitch >= chunk_len).
@@ -116,7 +125,12 @@ int bt_sha1_fill_synthetic(void *d_buf, uint64_t nbytes, uint64_t first_word, ui
 int bt_sha1_host_register(void *h_ptr, uint64_t len);
 int bt_sha1_host_unregister(void *h_ptr);
 /* make_chunks over a memory image: chunk i = h_in[i*chunk_len ..], the last
- * one may be short.  Returns the chunk count (ceil(total_len/chunk_len)). */
+ * one may be short.  Returns the chunk count (ceil(total_len/chunk_len)).
+ * Memory kept between calls: each device's context keeps its two staging
+ * lanes, grown on demand and reused by later calls -- up to 2 x 1 GiB of
+ * page-locked host memory (pageable input) and 2 x 1 GiB of HBM.  Pinned or
+ * registered input is DMA'd in bigger batches (BT_SHA1_DMA_BATCH_MB, 4 GiB
+ * by default); those HBM batches are freed before the call returns. */
 int64_t bt_sha1_chunks_host(const void *h_in, uint64_t total_len, uint64_t chunk_len,
                             uint8_t *h_digests);
 /* The same split over the first `ndev` GPUs (<=0: all), one host thread per
@@ -127,7 +141,9 @@ int64_t bt_sha1_chunks_host_multi(const void *h_in, uint64_t total_len, uint64_t
  * worker g takes chunks [g*n/G, (g+1)*n/G)).  An id may repeat: each repeat
  * is an independent worker (own host thread, streams and staging) on that
  * device, so the multi-GPU split / staging / ordered gather can be run with
- * any worker count on one GPU.  Returns the chunk count. */
+ * any worker count on one GPU.  The first use of a device works in its shared
+ * context (kept, as above); the repeats' contexts are freed before the call
+ * returns.  At most 64 workers.  Returns the chunk count. */
 int64_t bt_sha1_chunks_host_devices(const void *h_in, uint64_t total_len, uint64_t chunk_len,
                                     uint8_t *h_digests, const int *devs, int nworkers);
 /* make_chunks over a FILE* with an explicit chunk size (make_chunks uses

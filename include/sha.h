@@ -7,7 +7,7 @@
  * public layout (96 bytes: sha.h:39-50, little-endian default, no
  * RUNTIME_ENDIAN field): hash[] is the chaining state, buffer/bufferLength the
  * byte staging, totalLength the running bit count.  The compression itself
- * runs on the GPU (k_sha1_midstate); see bt_sha1.h for the batch API that
+ * runs on the GPU (k_sha1_chain in midstate mode); see bt_sha1.h for the batch API that
  * should be preferred for more than one message.
  */
 #ifndef _SHA1_H

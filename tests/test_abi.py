@@ -68,6 +68,19 @@ def test_dropin_void_calls_abort_without_gpu(tmp_path):
     assert "libbtsha1: shahash" in r.stderr
 
 
+def test_barrier_tallies_only_in_the_debug_build():
+    """bt_sha1_debug_barrier_stats reports -1 in the production library (no HIP
+    call is made); the barrier-accounting build (make dbgbar, exercised by
+    tests/test_gpu_barriers.py) carries the device tallies."""
+    bt = load_btsha1()
+    with pytest.raises(bt.BtSha1Error, match="dbgbar"):
+        bt.debug_barrier_stats()
+    dbg = os.path.join(REPO, "build_variants", "dbgbar", "libbtsha1.so")
+    assert os.path.exists(dbg), "run make dbgbar first"
+    assert b"g_bar_stats" in open(dbg, "rb").read()
+    assert b"g_bar_stats" not in open(LIB, "rb").read()
+
+
 def test_sha1context_layout_matches_reference():
     bt = load_btsha1()
     # sha.h:39-50 of the reference: u64 + 5*u32 + u32 + 64-byte union = 96 bytes

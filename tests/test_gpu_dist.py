@@ -10,6 +10,14 @@ the gloo control plane).  The ranks together hash global chunks 0..4095, so
 rank 0's `parity_first_4096_vs_golden` checks every rank's digests AND the
 gather order against the reference's golden vectors (tests/golden/synth4096.txt,
 produced by sha.c) -- config 4's split at a size one GPU holds.
+
+Those per-rank sizes (512..2048 chunks) select the latency kernels, so the
+second test runs the rank path at a per-rank size that selects the HOT kernel
+(k_sha1_fixed, > 128 chunks per CU): 2 ranks x 40960 chunks (2 x 20 GiB on the
+one MI355X), with the line's `digest_sample` -- first, middle and last chunk of
+EVERY rank by global index -- recomputed by the oracle on regenerated chunks,
+so rank 1's chunks 40960..81919 (far past the golden range) are checked too.
+chunk.c:20-21 carries no state between chunks, hence the contiguous split.
 """
 import json
 import os
@@ -22,6 +30,7 @@ import pytest
 from conftest import REPO
 
 pytestmark = pytest.mark.gpu
+CHUNK = 512 * 1024
 
 
 def _free_port():
@@ -30,19 +39,35 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_bench_ranks_split_and_gather_on_one_gpu(world):
-    chunks = 4096 // world
+def _run_bench(world, chunks, *extra, timeout=240):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(REPO, "bench.py"), "--gpus", str(world), "--chunks", str(chunks),
-           "--steps", "3", "--warmup", "1"]
-    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+           "--steps", "3", "--warmup", "1", *extra]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]  # rank 0 alone prints the line
-    line = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+def _check_sample(line, world, chunks, oracle):
+    """Every rank's sampled digests == the oracle on the regenerated chunk."""
+    sample = line["digest_sample"]
+    assert sorted({s["rank"] for s in sample}) == list(range(world))
+    for r in range(world):
+        got = sorted(s["chunk"] for s in sample if s["rank"] == r)
+        assert got[0] == r * chunks and got[-1] == (r + 1) * chunks - 1, got
+    for s in sample:
+        data = bytes(oracle.fill_synthetic(CHUNK, s["chunk"] * (CHUNK // 8), oracle.SEED_SYNTH))
+        assert oracle.sha1(data).hex() == s["sha1"], s
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_ranks_split_and_gather_on_one_gpu(world, oracle):
+    chunks = 4096 // world
+    line = _run_bench(world, chunks)
     assert line["n_gpus"] == world and line["steps"] == 3 and line["warmup"] == 1
     assert line["config"]["global_chunks"] == 4096
     assert line["parity_first_4096_vs_golden"] is True
@@ -53,3 +78,16 @@ def test_bench_ranks_split_and_gather_on_one_gpu(world):
     assert line["cpu_baseline"] is None and line["host_path"] is None
     # every rank read its own GPU's board power after the timed region
     assert [p["rank"] for p in line["power"]["per_gpu"]] == list(range(world))
+    _check_sample(line, world, chunks, oracle)
+
+
+def test_bench_ranks_run_the_hot_kernel_with_parity_on_every_rank(oracle):
+    """Config 4's per-rank kernel through the rank path: at 40960 chunks per
+    rank the batch selects k_sha1_fixed, as the 8-GPU bench's 131072 does."""
+    world, chunks = 2, 40960
+    line = _run_bench(world, chunks, "--power-s", "0", timeout=300)
+    assert line["roofline"]["kernel"] == "k_sha1_fixed"
+    assert line["config"]["global_chunks"] == world * chunks
+    assert line["parity_first_4096_vs_golden"] is True   # rank 0's first 4096 vs sha.c golden
+    assert [p["rank"] for p in line["per_gpu"]] == [0, 1]
+    _check_sample(line, world, chunks, oracle)

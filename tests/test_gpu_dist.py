@@ -14,7 +14,7 @@ produced by sha.c) -- config 4's split at a size one GPU holds.
 Those per-rank sizes (512..2048 chunks) select the latency kernels, so the
 second test runs the rank path at a per-rank size that selects the HOT kernel
 (k_sha1_fixed, > 128 chunks per CU): 2 ranks x 40960 chunks (2 x 20 GiB on the
-one MI355X), with the line's `digest_sample` -- first, middle and last chunk of
+one MI355X) and 2 ranks x 131072 chunks (config 4's exact per-rank size), with the line's `digest_sample` -- first, middle and last chunk of
 EVERY rank by global index -- recomputed by the oracle on regenerated chunks,
 so rank 1's chunks 40960..81919 (far past the golden range) are checked too.
 chunk.c:20-21 carries no state between chunks, hence the contiguous split.
@@ -81,10 +81,13 @@ def test_bench_ranks_split_and_gather_on_one_gpu(world, oracle):
     _check_sample(line, world, chunks, oracle)
 
 
-def test_bench_ranks_run_the_hot_kernel_with_parity_on_every_rank(oracle):
+@pytest.mark.parametrize("chunks", [40960, 131072])
+def test_bench_ranks_run_the_hot_kernel_with_parity_on_every_rank(oracle, chunks):
     """Config 4's per-rank kernel through the rank path: at 40960 chunks per
-    rank the batch selects k_sha1_fixed, as the 8-GPU bench's 131072 does."""
-    world, chunks = 2, 40960
+    rank the batch selects k_sha1_fixed (one-wave workgroups, < 1 wave per
+    SIMD), and 131072 per rank is exactly the 8-GPU bench's per-rank workload
+    (64 GiB each, 128 GiB for both ranks in the one GPU's 288 GB)."""
+    world = 2
     line = _run_bench(world, chunks, "--power-s", "0", timeout=300)
     assert line["roofline"]["kernel"] == "k_sha1_fixed"
     assert line["config"]["global_chunks"] == world * chunks

@@ -35,6 +35,10 @@ for step in "$@"; do
     tests) run pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     tests_new) run pytest_gpu_new 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
       -k "multi_device or null_stream or kernel_name or clock_probe or save_chunk" ;;
+    pytest:*)
+      # a subset of the gpu suite: pytest:<-k expression>
+      run "pytest_${step#pytest:}" 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        -p no:cacheprovider -k "${step#pytest:}" ;;
     bench) run bench 600 python3 bench.py ;;
     bench_rings)
       for r in 2 3 4; do run bench_ring$r 300 python3 bench.py --ring $r --steps 10 --no-cpu-baseline; done ;;

@@ -476,11 +476,14 @@ def main():
 
     clock = None
     if world == 1 and not args.no_clock and kernel == "k_sha1_fixed":
-        mhz, same = hasher.clock_mhz()
-        clock = {"in_kernel_mhz": round(mhz, 1), "probe_digests_identical": same,
-                 "method": "stamped build of the hot kernel (bt_sha1_clock_probe): median over waves of "
-                           "delta s_memtime / delta s_memrealtime x wall-clock rate, 3 launches after the "
-                           "timed region"}
+        try:
+            mhz, same = hasher.clock_mhz()
+            clock = {"in_kernel_mhz": round(mhz, 1), "probe_digests_identical": same,
+                     "method": "stamped build of the hot kernel (bt_sha1_clock_probe): median over waves of "
+                               "delta s_memtime / delta s_memrealtime x wall-clock rate, 3 launches after the "
+                               "timed region"}
+        except Exception as e:  # noqa: BLE001 -- the clock evidence must never cost the bench line
+            clock = {"error": f"{type(e).__name__}: {e}"}
 
     # Every rank measures its own GPU's power (all ranks run the window together).
     power = None
@@ -520,11 +523,8 @@ def main():
         # regenerated chunks, covering ranks >= 1 beyond the golden range.
         sample = None
         if args.digest_sample > 0:
-            sample, k = [], args.digest_sample
-            for r in range(world):
-                lo, hi = shard.weak_range(r, C)
-                picks = sorted({lo + (hi - 1 - lo) * j // max(1, k - 1) for j in range(k)})
-                sample += [{"rank": r, "chunk": g, "sha1": all_dig[20 * g:20 * g + 20].hex()} for g in picks]
+            sample = [{"rank": r, "chunk": g, "sha1": all_dig[20 * g:20 * g + 20].hex()}
+                      for r, g in shard.sample_chunks(world, C, args.digest_sample)]
 
         # PMC traffic, only when measured on this very build and layout.
         traffic, traffic_note = None, None
@@ -574,7 +574,8 @@ def main():
             except Exception as e:
                 host = {"error": f"{type(e).__name__}: {e}"}
 
-        peak_at_clock = VALU_MIX_PEAK_TOPS * (clock["in_kernel_mhz"] / 1000.0 / CLOCK_GHZ) if clock else None
+        peak_at_clock = (VALU_MIX_PEAK_TOPS * (clock["in_kernel_mhz"] / 1000.0 / CLOCK_GHZ)
+                         if clock and "in_kernel_mhz" in clock else None)
         line = {
             "metric": METRIC,
             "value": round(value, 3),

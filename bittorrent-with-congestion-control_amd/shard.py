@@ -27,6 +27,18 @@ def block_range(n, world, rank):
     return n * rank // world, n * (rank + 1) // world
 
 
+def sample_chunks(world, chunks_per_rank, k):
+    """(rank, global chunk index) of k chunks of every rank under weak scaling:
+    the rank's first and last chunk and k-2 evenly between (bench.py's
+    `digest_sample`, checked against the oracle by the tests)."""
+    out = []
+    for r in range(world):
+        lo, hi = weak_range(r, chunks_per_rank)
+        picks = sorted({lo + (hi - 1 - lo) * j // max(1, k - 1) for j in range(k)}) if hi > lo and k > 0 else []
+        out += [(r, g) for g in picks]
+    return out
+
+
 def barrier(world, group=None):
     if world > 1:
         import torch.distributed as dist

@@ -158,3 +158,42 @@ def test_block_range_covers_exactly():
             assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
     # weak scaling at 8 GPUs = BASELINE config 4's 1 M chunks
     assert shard.weak_range(7, 131072) == (917504, 1048576)
+
+
+def test_digest_sample_covers_every_rank_edges():
+    """bench.py's digest_sample picks: first and last chunk of EVERY rank (so
+    ranks >= 1, beyond the golden range, are checked), evenly between."""
+    shard = _load_shard()
+    got = shard.sample_chunks(8, 131072, 3)
+    assert [r for r, _ in got] == [r for r in range(8) for _ in range(3)]
+    for r in range(8):
+        mine = [g for rr, g in got if rr == r]
+        assert mine == [r * 131072, r * 131072 + 65535, (r + 1) * 131072 - 1]
+    assert shard.sample_chunks(2, 1, 3) == [(0, 0), (1, 1)]  # one chunk per rank: no duplicates
+    assert shard.sample_chunks(2, 5, 0) == []
+
+
+def test_bench_cpu_baseline_leg(oracle):
+    """bench.py's cpu_baseline leg on CPU: sustained medians, `cores` = the
+    usable CPU budget (affinity capped by the cgroup quota), thread counts
+    reported separately, and the reference's digests compared with the
+    (here: oracle-made) device digests."""
+    import ctypes
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    n, chunk = 8, 512 * 1024
+    data = bytes(oracle.fill_synthetic(n * chunk, 0, oracle.SEED_SYNTH))
+    buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
+    want = b"".join(oracle.hash_chunks(data, chunk))
+    cb = bench.cpu_baseline(ctypes.addressof(buf), n, want, min_s=0.05, reps=2)
+    cores, _, quota = bench.usable_cores()
+    assert cb["cores"] == cores and cb["threads"] == cores
+    assert cb["kind"] in ("reference", "port") and cb["digests_match_gpu"] is True
+    assert cb["value"] == cb["runs"][f"O2_{cores}t"]["GiB_per_s"] > 0
+    assert {"O2_1t", "O0_1t"} <= set(cb["runs"]) and cb["per_core_GiB_per_s_O2"] > 0
+    assert all(r["passes"] >= 2 for r in cb["runs"].values())  # repeated until >= min_s, twice
+    assert cb["runs"]["O2_1t"]["sample_chunks"] == n  # small sample: the 1-thread leg keeps all of it
+    bad = bytearray(want)
+    bad[0] ^= 1
+    assert bench.cpu_baseline(ctypes.addressof(buf), n, bytes(bad), min_s=0.01, reps=1)["digests_match_gpu"] is False

@@ -68,6 +68,16 @@ def test_dropin_void_calls_abort_without_gpu(tmp_path):
     assert "libbtsha1: shahash" in r.stderr
 
 
+def test_worker_list_is_bounded():
+    """bt_sha1_chunks_host_devices: each worker is a host thread with its own
+    staging lanes, so the list is capped (checked before any device call)."""
+    bt = load_btsha1()
+    with pytest.raises(bt.BtSha1Error, match="at most 64"):
+        bt.chunks_host(b"x" * 100, 64, devs=[0] * 65)
+    with pytest.raises(bt.BtSha1Error, match="empty device list"):
+        bt.chunks_host(b"x" * 100, 64, devs=[])
+
+
 def test_barrier_tallies_only_in_the_debug_build():
     """bt_sha1_debug_barrier_stats reports -1 in the production library (no HIP
     call is made); the barrier-accounting build (make dbgbar, exercised by

@@ -526,6 +526,12 @@ def main():
             sample = [{"rank": r, "chunk": g, "sha1": all_dig[20 * g:20 * g + 20].hex()}
                       for r, g in shard.sample_chunks(world, C, args.digest_sample)]
 
+        # A checksum of ALL digests in global chunk order (SHA-1 of the
+        # concatenated 20-byte digests, hashlib): the tests compare it with the
+        # oracle's digests of every regenerated chunk of every rank.
+        import hashlib
+        digests_sha1 = hashlib.sha1(all_dig).hexdigest() if all_dig else None
+
         # PMC traffic, only when measured on this very build and layout.
         traffic, traffic_note = None, None
         if os.path.exists(args.traffic_json):
@@ -619,6 +625,7 @@ def main():
                          "kernel_ms": round(k, 4)} for r, (w, k) in enumerate(res["per_rank"])],
             "parity_first_4096_vs_golden": parity,
             "digest_sample": sample,
+            "digests_sha1": digests_sha1,
             "cpu_baseline": cpu,
             "host_path": host,
         }

@@ -25,6 +25,8 @@ void or_hex2binary(const char *hex, int len, uint8_t *buf);
 void or_fill_synthetic(uint8_t *buf, uint64_t nbytes, uint64_t first_word, uint64_t seed);
 int or_hash_chunks(const uint8_t *base, uint64_t n, uint64_t pitch, uint32_t chunk_len, uint32_t last_len,
                    uint8_t *out, int nthreads);
+int or_synth_digests(uint64_t first_chunk, uint64_t n, uint32_t chunk_len, uint64_t seed, uint8_t *out,
+                     int nthreads);
 
 static int fails = 0;
 static void expect(const char *what, const uint8_t d[20], const char *hex) {
@@ -92,6 +94,22 @@ int main(void) {
     puts("FAIL short tail");
     fails++;
   }
+  /* regenerated synthetic chunks (per-thread scratch) == hashing the image */
+  const uint64_t first = 5, m = 11;
+  uint8_t *img2 = malloc(m * L), *c1 = malloc(20 * m), *c2 = malloc(20 * m);
+  or_fill_synthetic(img2, m * L, first * (L / 8), 77);
+  or_hash_chunks(img2, m, L, L, L, c1, 1);
+  if (or_synth_digests(first, m, L, 77, c2, 4) || memcmp(c1, c2, 20 * m)) {
+    puts("FAIL synth digests");
+    fails++;
+  }
+  if (or_synth_digests(0, 1, 12, 77, c2, 1) != -1) {
+    puts("FAIL synth digests accepted a chunk length that is not a multiple of 8");
+    fails++;
+  }
+  free(img2);
+  free(c1);
+  free(c2);
   free(img);
   free(a);
   free(b);

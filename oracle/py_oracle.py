@@ -30,6 +30,8 @@ _lib.or_sha1_final.argtypes = [_vp, _vp]
 _lib.or_sha1_blocks.argtypes = [_vp, _vp, _u64]
 _lib.or_binary2hex.argtypes = [_vp, ctypes.c_int, ctypes.c_char_p]
 _lib.or_hex2binary.argtypes = [ctypes.c_char_p, ctypes.c_int, _vp]
+_lib.or_synth_digests.argtypes = [_u64, _u64, ctypes.c_uint32, _u64, _vp, ctypes.c_int]
+_lib.or_synth_digests.restype = ctypes.c_int
 
 SEED_SYNTH = 0x0B175EED
 SEED_EDGE = 0x5EED0001
@@ -90,6 +92,30 @@ def hash_chunks(data, chunk_len, pitch=None, nthreads=1, lib=None):
     _lib.or_hash_chunks(src, n, pitch, chunk_len, last, out, nthreads)
     raw = bytes(out)
     return [raw[20 * i:20 * i + 20] for i in range(n)]
+
+
+def usable_cpus():
+    """CPUs this process may actually use: the affinity mask capped by the
+    cgroup CPU quota (a GPU box shows 256 CPUs but pays for 16)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = max(1, min(n, -(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def synth_digests(first_chunk, n, chunk_len=CHUNK, seed=SEED_SYNTH, nthreads=None) -> bytes:
+    """20-byte digests of synthetic chunks first_chunk .. first_chunk+n-1 (chunk g
+    = stream words [g*chunk_len/8, ..), as bench.py and the tests lay them out),
+    each regenerated and hashed in C across threads: every digest of a 64 GiB
+    batch in seconds, with no image in memory."""
+    out = (ctypes.c_uint8 * max(20 * n, 1))()
+    if _lib.or_synth_digests(first_chunk, n, chunk_len, seed, out, nthreads or usable_cpus()):
+        raise ValueError("or_synth_digests failed (chunk_len must be a multiple of 8)")
+    return bytes(out)[:20 * n]
 
 
 def binary2hex(b) -> str:

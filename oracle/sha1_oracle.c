@@ -22,8 +22,11 @@
  *   chunk.c:13-25  make_chunks   -> or_hash_chunks (fixed-size chunks, short tail)
  *   chunk.c:55-83  binary2hex / hex2binary -> or_binary2hex / or_hex2binary
  * plus the frozen synthetic-data generator shared with the device kernel
- * (bt_sha1.h: bt_sha1_fill_synthetic) and a pthread batch driver for the
- * CPU baseline.
+ * (bt_sha1.h: bt_sha1_fill_synthetic), a pthread batch driver for the CPU
+ * baseline, and or_synth_digests: the digests of a whole range of synthetic
+ * chunks, each regenerated per thread (no image in memory), so the GPU tests
+ * can check every digest of a 64 GiB (config 3) or multi-rank (config 4)
+ * batch, not a sample.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -51,10 +54,12 @@ static inline uint32_t be32(const uint8_t *p) {
 static void or_compress(uint32_t h[5], const uint8_t *block) {
   uint32_t w[80];
   for (int t = 0; t < 16; t++) w[t] = be32(block + 4 * t);
-  for (int t = 16; t < 80; t++) w[t] = rol(w[t - 3] ^ w[t - 8] ^ w[t - 14] ^ w[t - 16], 1);
+  /* The loops stay loops; the unroll hints only let gcc resolve the round
+   * selection at compile time (+40 % for the bulk sweeps of or_synth_digests). */
+  _Pragma("GCC unroll 64") for (int t = 16; t < 80; t++) w[t] = rol(w[t - 3] ^ w[t - 8] ^ w[t - 14] ^ w[t - 16], 1);
 
   uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
-  for (int t = 0; t < 80; t++) {
+  _Pragma("GCC unroll 80") for (int t = 0; t < 80; t++) {
     uint32_t f, k;
     if (t < 20) {
       f = d ^ (b & (c ^ d));
@@ -228,4 +233,58 @@ int or_hash_chunks(const uint8_t *base, uint64_t n, uint64_t pitch, uint32_t chu
   free(th);
   free(jobs);
   return 0;
+}
+
+/* ---- digests of synthetic chunks, regenerated on the fly ---------------------
+ * Chunk g (global index) of chunk_len bytes = stream words [g*chunk_len/8, ..)
+ * (chunk_len a multiple of 8, as bench.py lays chunks out at pitch = length).
+ * out[20*i ..] = shahash of chunk first_chunk + i, i < n; nthreads pthreads,
+ * each regenerating its chunks into its own chunk_len-byte scratch buffer. */
+typedef struct {
+  uint64_t first, lo, hi, seed;
+  uint32_t chunk_len;
+  uint8_t *out;
+  int err;
+} or_synth_job;
+
+static void *or_synth_worker(void *arg) {
+  or_synth_job *j = (or_synth_job *)arg;
+  uint8_t *buf = (uint8_t *)malloc(j->chunk_len ? j->chunk_len : 1);
+  if (!buf) {
+    j->err = 1;
+    return NULL;
+  }
+  for (uint64_t i = j->lo; i < j->hi; i++) {
+    or_fill_synthetic(buf, j->chunk_len, (j->first + i) * (j->chunk_len / 8), j->seed);
+    or_shahash(buf, (int)j->chunk_len, j->out + 20 * i);
+  }
+  free(buf);
+  return NULL;
+}
+
+int or_synth_digests(uint64_t first_chunk, uint64_t n, uint32_t chunk_len, uint64_t seed, uint8_t *out,
+                     int nthreads) {
+  if (chunk_len % 8) return -1;
+  if (nthreads < 1) nthreads = 1;
+  if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  or_synth_job *jobs = (or_synth_job *)calloc((size_t)nthreads, sizeof(or_synth_job));
+  if (!th || !jobs) {
+    free(th);
+    free(jobs);
+    return -1;
+  }
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (or_synth_job){first_chunk, n * t / nthreads, n * (t + 1) / nthreads, seed, chunk_len, out, 0};
+    if (t) pthread_create(&th[t], NULL, or_synth_worker, &jobs[t]);
+  }
+  or_synth_worker(&jobs[0]);
+  int err = jobs[0].err;
+  for (int t = 1; t < nthreads; t++) {
+    pthread_join(th[t], NULL);
+    err |= jobs[t].err;
+  }
+  free(th);
+  free(jobs);
+  return err ? -1 : 0;
 }

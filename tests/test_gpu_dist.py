@@ -16,9 +16,12 @@ second test runs the rank path at a per-rank size that selects the HOT kernel
 (k_sha1_fixed, > 128 chunks per CU): 2 ranks x 40960 chunks (2 x 20 GiB on the
 one MI355X) and 2 ranks x 131072 chunks (config 4's exact per-rank size), with the line's `digest_sample` -- first, middle and last chunk of
 EVERY rank by global index -- recomputed by the oracle on regenerated chunks,
-so rank 1's chunks 40960..81919 (far past the golden range) are checked too.
+so rank 1's chunks 40960..81919 (far past the golden range) are checked too;
+and the line's `digests_sha1` (a checksum of ALL gathered digests in global
+order) is compared with the oracle's digests of every chunk of every rank.
 chunk.c:20-21 carries no state between chunks, hence the contiguous split.
 """
+import hashlib
 import json
 import os
 import socket
@@ -62,6 +65,10 @@ def _check_sample(line, world, chunks, oracle):
     for s in sample:
         data = bytes(oracle.fill_synthetic(CHUNK, s["chunk"] * (CHUNK // 8), oracle.SEED_SYNTH))
         assert oracle.sha1(data).hex() == s["sha1"], s
+    # every digest of every rank, gathered in global order: the line's checksum
+    # of all of them == the oracle's over every regenerated chunk
+    want = oracle.synth_digests(0, world * chunks)
+    assert hashlib.sha1(want).hexdigest() == line["digests_sha1"]
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])

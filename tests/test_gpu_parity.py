@@ -477,8 +477,10 @@ def test_verifier_lifecycle_and_staging_growth(bt, oracle):
 
 
 def test_full_size_config3_properties(bt, torch, oracle):
-    """BASELINE config 3 size (131072 x 512 KiB = 64 GiB in HBM): spot parity
-    against the oracle on regenerated host data, determinism, distinctness."""
+    """BASELINE config 3 size (131072 x 512 KiB = 64 GiB in HBM): EVERY digest
+    equal to the oracle's on the chunk regenerated on the host (threaded C
+    sweep, oracle.synth_digests), plus determinism, distinctness and the
+    reference's golden digests for the first 4096."""
     n = 131072
     try:
         buf = torch.empty(n * CHUNK, dtype=torch.uint8, device="cuda")
@@ -500,6 +502,9 @@ def test_full_size_config3_properties(bt, torch, oracle):
     sample = list(range(n - 64, n)) + list(range(4096, n, 1024))
     for i in sample:
         assert dig[i] == oracle.sha1(bytes(oracle.fill_synthetic(CHUNK, i * 65536, oracle.SEED_SYNTH))), i
+    want = oracle.synth_digests(0, n)  # all 131072, ~10 s on the box's 16 CPUs
+    bad = [i for i in range(n) if raw[20 * i:20 * i + 20] != want[20 * i:20 * i + 20]]
+    assert not bad, (len(bad), bad[:10])
 
 
 def test_registered_host_image_direct_dma(bt, oracle):

@@ -85,6 +85,20 @@ def test_synth4096_sample(oracle):
         assert rows[i] == (str(i), oracle.sha1(data).hex())
 
 
+def test_synth_digests_equal_every_golden_row(oracle):
+    """The bulk sweep the GPU tests check whole batches with (each chunk
+    regenerated in C, threaded) reproduces ALL 4096 digests the compiled
+    reference produced (tests/golden/synth4096.txt), and equals hashing the
+    generated image for other chunk sizes and first chunks."""
+    rows = read_pairs("synth4096.txt")
+    d = oracle.synth_digests(0, 4096)
+    assert [(str(i), d[20 * i:20 * i + 20].hex()) for i in range(4096)] == rows
+    img = oracle.fill_synthetic(9 * 4096, 1000 * 512, 31)
+    assert oracle.synth_digests(1000, 9, 4096, 31, nthreads=3) == b"".join(oracle.hash_chunks(img, 4096))
+    with pytest.raises(ValueError):
+        oracle.synth_digests(0, 1, 12)
+
+
 def test_generator_matches_numpy_splitmix(oracle):
     """The frozen generator (shared with the device kernel) restated in numpy."""
     def splitmix(x):

@@ -531,6 +531,15 @@ def main():
         # oracle's digests of every regenerated chunk of every rank.
         import hashlib
         digests_sha1 = hashlib.sha1(all_dig).hexdigest() if all_dig else None
+        # ... and against the REFERENCE's checksum for this many global chunks
+        # (tests/golden/synth_checksums.txt, sha.c's digests of the same
+        # chunks): every digest of the run, every rank, in one comparison.
+        parity_all = None
+        sums = os.path.join(HERE, "tests", "golden", "synth_checksums.txt")
+        if digests_sha1 and os.path.exists(sums):
+            table = dict(l.split() for l in open(sums) if l.strip() and not l.startswith("#"))
+            if str(world * C) in table:
+                parity_all = table[str(world * C)] == digests_sha1
 
         # PMC traffic, only when measured on this very build and layout.
         traffic, traffic_note = None, None
@@ -626,6 +635,7 @@ def main():
             "parity_first_4096_vs_golden": parity,
             "digest_sample": sample,
             "digests_sha1": digests_sha1,
+            "parity_all_vs_golden": parity_all,
             "cpu_baseline": cpu,
             "host_path": host,
         }

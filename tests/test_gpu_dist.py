@@ -69,6 +69,9 @@ def _check_sample(line, world, chunks, oracle):
     # of all of them == the oracle's over every regenerated chunk
     want = oracle.synth_digests(0, world * chunks)
     assert hashlib.sha1(want).hexdigest() == line["digests_sha1"]
+    # and bench.py's own comparison with the reference's checksum for this
+    # global chunk count (tests/golden/synth_checksums.txt, from sha.c)
+    assert line["parity_all_vs_golden"] is True
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])

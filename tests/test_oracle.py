@@ -99,6 +99,19 @@ def test_synth_digests_equal_every_golden_row(oracle):
         oracle.synth_digests(0, 1, 12)
 
 
+def test_batch_checksums_are_the_reference_digests(oracle):
+    """tests/golden/synth_checksums.txt (the reference's digests of the bench's
+    synthetic chunks, checksummed per global chunk count): its 4096 row agrees
+    with the 4096 golden digests, and the oracle's sweep reproduces the
+    smaller rows; the config-4 row (1,048,576 chunks) is what bench.py's
+    parity_all_vs_golden compares an 8-GPU run with."""
+    table = dict(read_pairs("synth_checksums.txt"))
+    assert {"4096", "81920", "131072", "262144", "524288", "1048576"} <= set(table)
+    rows = read_pairs("synth4096.txt")
+    assert hashlib.sha1(b"".join(bytes.fromhex(h) for _, h in rows)).hexdigest() == table["4096"]
+    assert hashlib.sha1(oracle.synth_digests(0, 81920)).hexdigest() == table["81920"]
+
+
 def test_generator_matches_numpy_splitmix(oracle):
     """The frozen generator (shared with the device kernel) restated in numpy."""
     def splitmix(x):

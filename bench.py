@@ -328,14 +328,19 @@ def cpu_baseline(host_addr, n_chunks, gpu_digests, min_s=1.0, reps=3):
         for nt in sorted(counts):
             r = run(fn, nt, n1 if nt == 1 else n_chunks)
             rows[f"{opt}_{nt}t"] = {**r, "threads": nt, "flags": flags, "kind": k}
-    head = rows.get(f"O2_{cores}t") or next(iter(rows.values()))
+    # value: the best sustained -O2 rate over the multi-thread runs (`cores`
+    # threads, one per CPU of the affinity mask); both are bounded by the
+    # quota, and with exactly `cores` threads the process's other threads
+    # (interpreter, HIP runtime) make that run the noisier of the two.
+    multi = [r for key, r in rows.items() if key.startswith("O2_") and r["threads"] > 1]
+    head = max(multi, key=lambda r: r["GiB_per_s"]) if multi else (rows.get("O2_1t") or next(iter(rows.values())))
     per_core = rows.get("O2_1t", {}).get("GiB_per_s")
     return {
         "value": head["GiB_per_s"], "unit": "GiB/s", "cores": cores, "threads": head["threads"], "kind": kind,
         "sample": f"{n_chunks} x 512 KiB chunks ({n_chunks * CHUNK / 2**30:.1f} GiB) of the benchmark's own "
                   f"synthetic chunks ({n1} on 1 thread), shahash per chunk (chunk.c:21), static split; each "
-                  f"rate = median of {reps} measurements of >= {min_s:g} s; value = -O2 on `cores` threads "
-                  f"(= min(affinity {affinity}, ceil(cgroup quota {quota})))",
+                  f"rate = median of {reps} measurements of >= {min_s:g} s; value = the best -O2 rate with "
+                  f"`cores` (= min(affinity {affinity}, ceil(cgroup quota {quota}))) or {affinity} threads",
         "flags": head["flags"], "digests_match_gpu": all(r["digests_match_gpu"] for r in rows.values()),
         "per_core_GiB_per_s_O2": per_core,
         "quota_bound_GiB_per_s": round(per_core * quota, 3) if per_core and quota else None,

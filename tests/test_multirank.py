@@ -188,9 +188,13 @@ def test_bench_cpu_baseline_leg(oracle):
     want = b"".join(oracle.hash_chunks(data, chunk))
     cb = bench.cpu_baseline(ctypes.addressof(buf), n, want, min_s=0.05, reps=2)
     cores, _, quota = bench.usable_cores()
-    assert cb["cores"] == cores and cb["threads"] == cores
+    assert cb["cores"] == cores
     assert cb["kind"] in ("reference", "port") and cb["digests_match_gpu"] is True
-    assert cb["value"] == cb["runs"][f"O2_{cores}t"]["GiB_per_s"] > 0
+    multi = [r for k, r in cb["runs"].items() if k.startswith("O2_") and r["threads"] > 1]
+    if multi:  # the best multi-thread -O2 run, its thread count reported beside `cores`
+        best = max(multi, key=lambda r: r["GiB_per_s"])
+        assert cb["value"] == best["GiB_per_s"] > 0 and cb["threads"] == best["threads"]
+        assert f"O2_{cores}t" in cb["runs"]
     assert {"O2_1t", "O0_1t"} <= set(cb["runs"]) and cb["per_core_GiB_per_s_O2"] > 0
     assert all(r["passes"] >= 2 for r in cb["runs"].values())  # repeated until >= min_s, twice
     assert cb["runs"]["O2_1t"]["sample_chunks"] == n  # small sample: the 1-thread leg keeps all of it

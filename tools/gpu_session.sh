@@ -40,6 +40,9 @@ for step in "$@"; do
       run "pytest_${step#pytest:}" 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "${step#pytest:}" ;;
     bench) run bench 600 python3 bench.py ;;
+    bench2)
+      # two default runs back to back on one box (within-box repeatability of the line)
+      run bench_a 600 python3 bench.py && run bench_b 600 python3 bench.py ;;
     bench_rings)
       for r in 2 3 4; do run bench_ring$r 300 python3 bench.py --ring $r --steps 10 --no-cpu-baseline; done ;;
     prof)

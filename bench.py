@@ -125,6 +125,33 @@ class DeviceHasher:
     def digests(self):
         return self.dig.cpu().numpy().tobytes()
 
+    def verify_rate(self, reps=5):
+        """Device-resident verify (util.c:311-313's hash + memcmp, batched):
+        bt_sha1_verify_dev over the same chunks against expected digests in
+        HBM, every 997th deliberately wrong; HIP-event time per pass on the
+        hasher's stream and whether exactly the wrong ones were flagged."""
+        torch = self.torch
+        with torch.cuda.stream(self.stream):
+            exp = self.dig.clone()
+            bad = torch.arange(0, self.C, 997, device="cuda")
+            exp.view(-1, 20)[bad, 0] ^= 1
+            ok = torch.full((self.C,), 7, dtype=torch.uint8, device="cuda")
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(self.stream)
+            for _ in range(reps):
+                self.bt.verify_dev(self.buf.data_ptr(), self.C, CHUNK, self.pitch, exp.data_ptr(), ok.data_ptr(),
+                                   None, self.sp)
+            b.record(self.stream)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / reps
+        want = torch.ones(self.C, dtype=torch.uint8, device="cuda")
+        want[bad] = 0
+        return {"GiB_per_s": round(self.C * CHUNK / (ms * 1e-3) / 2**30, 3), "kernel_ms": round(ms, 4),
+                "flags_correct": bool(torch.equal(ok, want)), "mismatches_planted": int(bad.numel()),
+                "kernel": self.bt.kernel_name(self.C),
+                "path": "bt_sha1_verify_dev: the hot kernel with its fused compare epilogue (util.c:311-313) "
+                        "against expected digests in HBM, one launch per pass"}
+
     def clock_mhz(self, launches=3):
         """Median in-kernel shader clock over the waves of the last of
         `launches` back-to-back launches of the stamped build, right after the
@@ -586,6 +613,13 @@ def main():
             except Exception as e:  # the checker must never cost the bench line
                 cpu = {"error": f"{type(e).__name__}: {e}"}
 
+        verify = None
+        if world == 1:
+            try:
+                verify = hasher.verify_rate()
+            except Exception as e:  # noqa: BLE001 -- never costs the bench line
+                verify = {"error": f"{type(e).__name__}: {e}"}
+
         host = None
         if world == 1 and not args.no_host_path and pitch == CHUNK:
             try:
@@ -642,6 +676,7 @@ def main():
             "digests_sha1": digests_sha1,
             "parity_all_vs_golden": parity_all,
             "cpu_baseline": cpu,
+            "verify_dev": verify,
             "host_path": host,
         }
         print(json.dumps(line), flush=True)

@@ -104,3 +104,23 @@ def test_bench_ranks_run_the_hot_kernel_with_parity_on_every_rank(oracle, chunks
     assert line["parity_first_4096_vs_golden"] is True   # rank 0's first 4096 vs sha.c golden
     assert [p["rank"] for p in line["per_gpu"]] == [0, 1]
     _check_sample(line, world, chunks, oracle)
+
+
+def test_bench_single_rank_line_checks(oracle):
+    """bench.py at N = 1 (plain `python bench.py`, as the driver runs it) at
+    config 2's 4096 chunks: parity against the reference's golden digests and
+    checksum, and the device-resident verify leg flags exactly the planted
+    mismatches (the fused compare of util.c:311-313)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--chunks", "4096", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline", "--no-host-path", "--power-s", "0"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and line["parity_first_4096_vs_golden"] is True
+    assert line["parity_all_vs_golden"] is True
+    v = line["verify_dev"]
+    assert v["flags_correct"] is True and v["mismatches_planted"] == len(range(0, 4096, 997)) and v["GiB_per_s"] > 0
+    _check_sample(line, 1, 4096, oracle)

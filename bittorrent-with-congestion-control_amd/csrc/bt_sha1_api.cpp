@@ -176,6 +176,7 @@ struct StageBuf {
 struct Lane {
   hipStream_t s = nullptr;
   hipEvent_t ev = nullptr;
+  hipEvent_t copied = nullptr;  // after the batch's last H2D (serial copy order)
   StageBuf h_in;  // staged input pieces, DMA'd to d_in
   PinBuf h_dig;   // the kernel stores digests straight into it
   DevBuf d_in;
@@ -239,6 +240,8 @@ void release_ctx(DevCtx *c) {
       (void)hipStreamDestroy(l.s);
     }
     if (l.ev) (void)hipEventDestroy(l.ev);
+    if (l.copied) (void)hipEventDestroy(l.copied);
+    l.copied = nullptr;
     l.s = nullptr;
     l.ev = nullptr;
     l.h_in.release();
@@ -259,6 +262,7 @@ int ensure_streams(DevCtx *c) {
   for (auto &l : c->lane) {
     BT_CK(hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking));
     BT_CK(hipEventCreateWithFlags(&l.ev, hipEventDisableTiming));
+    BT_CK(hipEventCreateWithFlags(&l.copied, hipEventDisableTiming));
   }
   c->s = c->lane[0].s;
   return 0;
@@ -444,6 +448,25 @@ double now_s() {
 
 constexpr uint64_t kPiece = 128ull << 20;  // staging -> H2D granule inside a batch
 
+// Copy order of the two lanes.  "serial": a batch's first H2D waits for the
+// previous batch's last one, so one copy runs at a time (hashing still
+// overlaps the next copy).  "overlap": a batch's H2D may run beside the
+// previous batch's (two DMA engines at once).  Default: serial for direct DMA
+// from pinned / registered memory, overlap for the staged lanes.  Measured
+// (tools/numa_probe.py 8, profiles/r03/numa_probe.md): an 8 GiB registered
+// image on the GPU's socket 50.6 (overlap) / 50.1 (serial) GiB/s, on the other
+// socket 42.2 (overlap) / 49.7 (serial) -- two concurrent DMA streams out of
+// the other socket's memory lose ~8 GiB/s; the staged lanes (whose pages the
+// copy threads place) lose ~1 with serial copies.  BT_SHA1_COPY_ORDER=
+// serial|overlap forces one order.
+bool serial_copies(bool staged) {
+  static const int forced = [] {
+    const char *e = getenv("BT_SHA1_COPY_ORDER");
+    return e ? (!strcmp(e, "serial") ? 1 : !strcmp(e, "overlap") ? 0 : -1) : -1;
+  }();
+  return forced >= 0 ? forced == 1 : !staged;
+}
+
 template <class Fill, class Sink>
 int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool staged, Fill fill, Sink sink) {
   if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
@@ -510,6 +533,7 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   for (;;) {
     Lane &l = c->lane[k & 1];
     if ((k == 1 && join_pre()) || drain(l) || prepare(l)) return -1;
+    if (k > 0 && serial_copies(staged)) BT_CK(hipStreamWaitEvent(l.s, c->lane[(k + 1) & 1].copied, 0));
     uint64_t got = 0;
     bool eof = false;
     while (got < bytes_per) {
@@ -530,6 +554,7 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
       }
     }
     if (got == 0) break;
+    if (serial_copies(staged)) BT_CK(hipEventRecord(l.copied, l.s));
     const uint64_t cnt = (got + chunk_len - 1) / chunk_len;
     if (launch_image(l.d_in.as<uint8_t>(), got, chunk_len, l.h_dig.as<uint8_t>(), l.s)) return -1;
     BT_CK(hipEventRecord(l.ev, l.s));

@@ -200,6 +200,20 @@ for step in "$@"; do
       run stream_prof 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/stream_prof" -o sb \
         -- python3 "$ROOT/tools/stream_bench.py" 4 ;;
     latency) run latency 300 python3 tools/latency_bench.py ;;
+    numa) run numa 600 python3 tools/numa_probe.py 4 ;;
+    numa_final)
+      for rep in 1 2; do
+        run "nf_default_$rep" 600 python3 tools/numa_probe.py 8 && \
+        run "nf_numa0_$rep" 600 env BT_SHA1_NUMA=0 python3 tools/numa_probe.py 8 || exit 1
+      done ;;
+    copy_order)
+      for rep in 1 2; do
+        run "co_overlap_$rep" 600 env BT_SHA1_NUMA=0 python3 tools/numa_probe.py 8 && \
+        run "co_serial_$rep" 600 env BT_SHA1_NUMA=0 BT_SHA1_COPY_ORDER=serial python3 tools/numa_probe.py 8 || exit 1
+      done ;;
+    numa_ab)
+      run numa_off 600 env BT_SHA1_NUMA=0 python3 tools/numa_probe.py 4 && run numa_on 600 python3 tools/numa_probe.py 4 \
+        && run numa_off8 600 env BT_SHA1_NUMA=0 python3 tools/numa_probe.py 8 && run numa_on8 600 python3 tools/numa_probe.py 8 ;;
     latency_ab)
       run latency_spin 300 python3 tools/latency_bench.py
       run latency_streamsync 300 env BT_SHA1_SYNC=stream python3 tools/latency_bench.py

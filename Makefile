@@ -90,11 +90,15 @@ ASANRT   := $(dir $(shell /opt/rocm/llvm/bin/clang -print-file-name=libclang_rt.
 ASANFLAGS := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer
 asan: $(ASANDIR)/host_stress
 
-$(ASANDIR)/libbtsha1.so: $(CSRC)/bt_sha1_api.cpp $(CSRC)/bt_chunks.cpp $(PKG)/build/sha1_kernels.o include/bt_sha1.h
+# The kernels carry only the default hot-kernel variant (-DBT_SHA1_ONE_VARIANT):
+# the ASan run never selects another, and this library travels with every lease.
+$(ASANDIR)/libbtsha1.so: $(CSRC)/bt_sha1_api.cpp $(CSRC)/bt_chunks.cpp $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h \
+                        $(CSRC)/sha1_launch.h include/bt_sha1.h
 	@mkdir -p $(ASANDIR)
-	$(HIPCC) $(HIPFLAGS) -gline-tables-only $(ASANFLAGS) -c $(CSRC)/bt_sha1_api.cpp -o $(ASANDIR)/bt_sha1_api.o
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_ONE_VARIANT -c $(CSRC)/sha1_kernels.hip -o $(ASANDIR)/sha1_kernels.o
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_SRC_ID='"$(SRC_ID)"' -gline-tables-only $(ASANFLAGS) -c $(CSRC)/bt_sha1_api.cpp -o $(ASANDIR)/bt_sha1_api.o
 	$(HIPCC) $(HIPFLAGS) -gline-tables-only $(ASANFLAGS) -c $(CSRC)/bt_chunks.cpp -o $(ASANDIR)/bt_chunks.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(PKG)/build/sha1_kernels.o $(ASANDIR)/bt_sha1_api.o $(ASANDIR)/bt_chunks.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(ASANDIR)/sha1_kernels.o $(ASANDIR)/bt_sha1_api.o $(ASANDIR)/bt_chunks.o
 
 $(ASANDIR)/host_stress: tests/native/host_stress.c $(ASANDIR)/libbtsha1.so
 	/opt/rocm/llvm/bin/clang -gline-tables-only -O1 -fsanitize=address,undefined -shared-libasan -fno-omit-frame-pointer -Iinclude -o $@ $< \
@@ -109,7 +113,7 @@ DBGDIR   := build_variants/dbgbar
 dbgbar: $(DBGDIR)/libbtsha1.so
 $(DBGDIR)/libbtsha1.so: $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h $(CSRC)/sha1_launch.h $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o
 	@mkdir -p $(DBGDIR)
-	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_DEBUG_BARRIERS -c $< -o $(DBGDIR)/sha1_kernels.o
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_DEBUG_BARRIERS -DBT_SHA1_ONE_VARIANT -c $< -o $(DBGDIR)/sha1_kernels.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(DBGDIR)/sha1_kernels.o $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o -Wl,-soname,libbtsha1.so
 
 # Scheduler-strategy builds of the library (experiment in profiles/r01/experiments.md;

@@ -1199,9 +1199,16 @@ uint64_t btsha1_latency_batch() {
 constexpr int kLdsVariant = 1010;  // bt_sha1_set_variant(10, 1, 0): LDS-staged k_sha1_lds
 constexpr int kLdsNtVariant = 1011;  // bt_sha1_set_variant(10, 1, 1): the same with nt DMA loads
 
-// Variant code: NBUF*100 + L*10 + (nt ? 1 : 0).
+// Variant code: NBUF*100 + L*10 + (nt ? 1 : 0).  The diagnostic builds
+// (make asan / dbgbar: -DBT_SHA1_ONE_VARIANT) carry only the default variant:
+// each hot-kernel instantiation is ~45 KB of code, and those libraries travel
+// with every GPU lease.
+#ifdef BT_SHA1_ONE_VARIANT
+#define BT_FIXED_VARIANTS(X) X(3, 1, 0)
+#else
 #define BT_FIXED_VARIANTS(X) X(2, 1, 0) X(3, 1, 0) X(4, 1, 0) X(2, 2, 0) \
   X(2, 1, 2) X(3, 1, 2) X(2, 2, 2)
+#endif
 
 bool btsha1_fixed_variant_ok(int code) {
   if (code == kLdsVariant || code == kLdsNtVariant) return true;

@@ -139,8 +139,23 @@ tools/ubench/%: tools/ubench/%.hip $(CSRC)/sha1_device.h
 tools/ubench/residency: tools/ubench/residency.cpp $(LIB)
 	$(HIPCC) -O2 -std=c++17 -I$(CSRC) -o $@ $< -L$(PKG) -lbtsha1 -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
 
+# Install the drop-in for a reference build to link against:
+#   make install PREFIX=/opt/btsha1  ->  lib/libbtsha1.so, include/{sha.h,chunk.h,bt_sha1.h},
+#   bin/{make-chunks,verify-stream}, lib/pkgconfig/btsha1.pc
+PREFIX   ?= /usr/local
+install: lib
+	install -d $(DESTDIR)$(PREFIX)/lib/pkgconfig $(DESTDIR)$(PREFIX)/include $(DESTDIR)$(PREFIX)/bin
+	install -m 755 $(LIB) $(DESTDIR)$(PREFIX)/lib/libbtsha1.so
+	install -m 644 include/sha.h include/chunk.h include/bt_sha1.h $(DESTDIR)$(PREFIX)/include/
+	gcc -O2 -Wall -Wextra -Iinclude -o $(DESTDIR)$(PREFIX)/bin/make-chunks $(PKG)/host/make_chunks_main.c \
+	    -L$(DESTDIR)$(PREFIX)/lib -lbtsha1 -Wl,-rpath,$(PREFIX)/lib
+	gcc -O2 -Wall -Wextra -Iinclude -o $(DESTDIR)$(PREFIX)/bin/verify-stream $(PKG)/host/verify_stream.c \
+	    -L$(DESTDIR)$(PREFIX)/lib -lbtsha1 -Wl,-rpath,$(PREFIX)/lib
+	printf 'prefix=%s\nlibdir=$${prefix}/lib\nincludedir=$${prefix}/include\n\nName: btsha1\nDescription: %s\nVersion: 3\nLibs: -L$${libdir} -lbtsha1 -Wl,-rpath,$${libdir}\nCflags: -I$${includedir}\n' \
+	    '$(PREFIX)' 'MI355X SHA-1 chunk hashing, drop-in for sha.h / chunk.h' > $(DESTDIR)$(PREFIX)/lib/pkgconfig/btsha1.pc
+
 clean:
 	rm -rf $(PKG)/build $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib tools oracle dropin asan dbgbar ubench sched_variants clean
+.PHONY: all lib tools oracle dropin asan dbgbar ubench sched_variants install clean

@@ -139,3 +139,31 @@ def test_integration_peer_example_compiles(tmp_path):
                         "-o", str(exe), str(src), f"-L{PKG}", "-lbtsha1", f"-Wl,-rpath,{PKG}"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_make_install_tree_links_a_reference_style_caller(tmp_path):
+    """`make install PREFIX=...` gives the layout a reference build links
+    against: the library, the drop-in headers, the CLIs
+    and a pkg-config file whose flags build a chunk.h / sha.h caller."""
+    prefix = tmp_path / "inst"
+    r = subprocess.run(["make", "-C", REPO, "install", f"PREFIX={prefix}"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    for f in ("lib/libbtsha1.so", "include/sha.h", "include/chunk.h", "include/bt_sha1.h",
+              "bin/make-chunks", "bin/verify-stream", "lib/pkgconfig/btsha1.pc"):
+        assert (prefix / f).exists(), f
+    pc = dict(l.split("=", 1) for l in (prefix / "lib/pkgconfig/btsha1.pc").read_text().splitlines()
+              if "=" in l and ":" not in l.split("=", 1)[0])
+    assert pc["prefix"] == str(prefix)
+    src = tmp_path / "caller.c"
+    src.write_text('#include <stdio.h>\n#include "chunk.h"\n#include "sha.h"\n'
+                   "int main(int c, char **v) { uint8_t *h[1]; uint8_t d[20]; SHA1Context s; SHA1Init(&s);\n"
+                   "  if (c > 5) { FILE *f = fopen(v[1], \"rb\"); h[0] = d; return make_chunks(f, h); }\n"
+                   "  return 0; }\n")
+    exe = tmp_path / "caller"
+    r = subprocess.run(["gcc", "-Wall", "-Werror", f"-I{prefix}/include", "-o", str(exe), str(src),
+                        f"-L{prefix}/lib", "-lbtsha1", f"-Wl,-rpath,{prefix}/lib"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    ldd = subprocess.run(["ldd", str(exe)], capture_output=True, text=True).stdout
+    assert f"{prefix}/lib/libbtsha1.so" in ldd
+    ldd = subprocess.run(["ldd", str(prefix / "bin" / "make-chunks")], capture_output=True, text=True).stdout
+    assert f"{prefix}/lib/libbtsha1.so" in ldd

@@ -22,7 +22,7 @@ BIN      := $(PKG)/bin
 
 REF      ?= /root/reference
 
-all: lib tools oracle dropin asan dbgbar
+all: lib tools oracle dropin asan dbgbar experiments
 
 lib: $(LIB)
 
@@ -90,13 +90,14 @@ ASANRT   := $(dir $(shell /opt/rocm/llvm/bin/clang -print-file-name=libclang_rt.
 ASANFLAGS := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer
 asan: $(ASANDIR)/host_stress
 
-# The kernels carry only the default hot-kernel variant (-DBT_SHA1_ONE_VARIANT):
-# the ASan run never selects another, and this library travels with every lease.
+# Like every build but `experiments`, the kernels carry only the default hot
+# kernel.  Each diagnostic build compiles the API object with its own suffixed
+# source id, so bench.py never credits it with the product's PMC traffic.
 $(ASANDIR)/libbtsha1.so: $(CSRC)/bt_sha1_api.cpp $(CSRC)/bt_chunks.cpp $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h \
                         $(CSRC)/sha1_launch.h include/bt_sha1.h
 	@mkdir -p $(ASANDIR)
-	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_ONE_VARIANT -c $(CSRC)/sha1_kernels.hip -o $(ASANDIR)/sha1_kernels.o
-	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_SRC_ID='"$(SRC_ID)"' -gline-tables-only $(ASANFLAGS) -c $(CSRC)/bt_sha1_api.cpp -o $(ASANDIR)/bt_sha1_api.o
+	$(HIPCC) $(HIPFLAGS) -c $(CSRC)/sha1_kernels.hip -o $(ASANDIR)/sha1_kernels.o
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_SRC_ID='"$(SRC_ID)-asan"' -gline-tables-only $(ASANFLAGS) -c $(CSRC)/bt_sha1_api.cpp -o $(ASANDIR)/bt_sha1_api.o
 	$(HIPCC) $(HIPFLAGS) -gline-tables-only $(ASANFLAGS) -c $(CSRC)/bt_chunks.cpp -o $(ASANDIR)/bt_chunks.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(ASANDIR)/sha1_kernels.o $(ASANDIR)/bt_sha1_api.o $(ASANDIR)/bt_chunks.o
 
@@ -111,10 +112,26 @@ $(ASANDIR)/host_stress: tests/native/host_stress.c $(ASANDIR)/libbtsha1.so
 # tests/test_gpu_barriers.py in a child process (BT_SHA1_LIB points at it).
 DBGDIR   := build_variants/dbgbar
 dbgbar: $(DBGDIR)/libbtsha1.so
-$(DBGDIR)/libbtsha1.so: $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h $(CSRC)/sha1_launch.h $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o
+$(DBGDIR)/libbtsha1.so: $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h $(CSRC)/sha1_launch.h $(CSRC)/bt_sha1_api.cpp \
+                        include/bt_sha1.h $(PKG)/build/bt_chunks.o
 	@mkdir -p $(DBGDIR)
-	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_DEBUG_BARRIERS -DBT_SHA1_ONE_VARIANT -c $< -o $(DBGDIR)/sha1_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(DBGDIR)/sha1_kernels.o $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o -Wl,-soname,libbtsha1.so
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_DEBUG_BARRIERS -c $< -o $(DBGDIR)/sha1_kernels.o
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_SRC_ID='"$(SRC_ID)-dbgbar"' -c $(CSRC)/bt_sha1_api.cpp -o $(DBGDIR)/bt_sha1_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(DBGDIR)/sha1_kernels.o $(DBGDIR)/bt_sha1_api.o $(PKG)/build/bt_chunks.o -Wl,-soname,libbtsha1.so
+
+# Experiments build: the hot-kernel variants measured and rejected (ring depth
+# 2 / 4, two-line slots, non-temporal loads, LDS-DMA staging)
+# beside the default, selected with bt_sha1_set_variant.  Not the product: the
+# product library carries only the default hot kernel.  Loaded (BT_SHA1_LIB)
+# by tests/test_gpu_variants.py in a child process and by bench.py --ring.
+EXPDIR   := build_variants/experiments
+experiments: $(EXPDIR)/libbtsha1.so
+$(EXPDIR)/libbtsha1.so: $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h $(CSRC)/sha1_launch.h $(CSRC)/bt_sha1_api.cpp \
+                        include/bt_sha1.h $(PKG)/build/bt_chunks.o
+	@mkdir -p $(EXPDIR)
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_EXPERIMENTS -c $< -o $(EXPDIR)/sha1_kernels.o
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_SRC_ID='"$(SRC_ID)-exp"' -c $(CSRC)/bt_sha1_api.cpp -o $(EXPDIR)/bt_sha1_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(EXPDIR)/sha1_kernels.o $(EXPDIR)/bt_sha1_api.o $(PKG)/build/bt_chunks.o -Wl,-soname,libbtsha1.so
 
 # Scheduler-strategy builds of the library (experiment in profiles/r01/experiments.md;
 # tools/gpu_session.sh libvariants benches each).  Not part of the product.
@@ -125,10 +142,11 @@ SCHED_maxmem  := -mllvm -amdgpu-sched-strategy=max-memory-clause
 SCHED_bias0   := -mllvm -amdgpu-schedule-metric-bias=0
 SCHED_NAMES   := default maxilp iterilp maxmem bias0
 sched_variants: $(foreach v,$(SCHED_NAMES),build_variants/$(v)/libbtsha1.so)
-build_variants/%/libbtsha1.so: $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o
+build_variants/%/libbtsha1.so: $(CSRC)/sha1_kernels.hip $(CSRC)/sha1_device.h $(CSRC)/bt_sha1_api.cpp $(PKG)/build/bt_chunks.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(SCHED_$*) -c $< -o $(dir $@)sha1_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(dir $@)sha1_kernels.o $(PKG)/build/bt_sha1_api.o $(PKG)/build/bt_chunks.o -Wl,-soname,libbtsha1.so
+	$(HIPCC) $(HIPFLAGS) -DBT_SHA1_SRC_ID='"$(SRC_ID)-sched-$*"' -c $(CSRC)/bt_sha1_api.cpp -o $(dir $@)bt_sha1_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(dir $@)sha1_kernels.o $(dir $@)bt_sha1_api.o $(PKG)/build/bt_chunks.o -Wl,-soname,libbtsha1.so
 
 # Microbenchmarks behind the measurements in profiles/ (not part of the product).
 UB_SRC := $(wildcard tools/ubench/*.hip)
@@ -158,4 +176,4 @@ clean:
 	rm -rf $(PKG)/build $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib tools oracle dropin asan dbgbar ubench sched_variants install clean
+.PHONY: all lib tools oracle dropin asan dbgbar experiments ubench sched_variants install clean

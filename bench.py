@@ -32,6 +32,7 @@ sets the hot kernel's clock).
 """
 import argparse
 import ctypes
+import glob
 import importlib.util
 import json
 import math
@@ -41,6 +42,8 @@ import sys
 import tempfile
 import threading
 import time
+
+_T_IMPORT = time.perf_counter()
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(HERE, "bittorrent-with-congestion-control_amd")
@@ -56,6 +59,23 @@ SIMDS, CLOCK_GHZ = 1024, 2.4
 _MIX_CLK = 4 * VALU_HALF_RATE_PER_BLOCK + 2 * VALU_FULL_RATE_PER_BLOCK
 VALU_MIX_PEAK_TOPS = VALU_OPS_PER_BLOCK * 64 * SIMDS * CLOCK_GHZ * 1e9 / _MIX_CLK / 1e12  # lane-ops/s, ~47.1
 METRIC = "GiB/s SHA-1 hashed (device-resident 512KiB chunks) at 1/2/4/8 MI355X"
+DEFAULT_VARIANT = (3, 1, 0)  # the product library's one hot kernel
+
+
+def process_age_s():
+    """Seconds since THIS process started (kernel start time from
+    /proc/self/stat against /proc/uptime, 1/CLK_TCK resolution), i.e. from
+    interpreter start -- what the driver's clock around `python bench.py` sees,
+    minus the exec.  Falls back to the time since bench.py was imported."""
+    try:
+        with open("/proc/self/stat") as f:
+            after_comm = f.read().rsplit(")", 1)[1].split()
+        start_ticks = int(after_comm[19])  # field 22 of stat(5); field 3 is after_comm[0]
+        with open("/proc/uptime") as f:
+            uptime = float(f.read().split()[0])
+        return round(uptime - start_ticks / os.sysconf("SC_CLK_TCK"), 2)
+    except (OSError, ValueError, IndexError):
+        return round(time.perf_counter() - _T_IMPORT, 2)
 
 
 def _load(name, path):
@@ -188,6 +208,34 @@ def _smi_handle(torch, dev):
         if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
             return amdsmi, h
     return amdsmi, None
+
+
+def device_identity(torch, dev):
+    """Which physical GPU this rank drives: its PCI address (domain:bus:device.0,
+    as HIP reports it) and the UUID amdsmi holds for that address (the
+    `uuid` HIP exposes through torch as a fallback), the HIP device index, and
+    how many devices the rank can see -- so an N > 1 line proves it ran on N
+    distinct GPUs (shard.check_distinct_devices)."""
+    p = torch.cuda.get_device_properties(dev)
+    ident = {"pci_bdf": f"{int(p.pci_domain_id):04x}:{int(p.pci_bus_id):02x}:{int(p.pci_device_id):02x}.0",
+             "uuid": None, "hip_device": dev, "device_count": torch.cuda.device_count(), "name": p.name}
+    smi = None
+    try:
+        smi, h = _smi_handle(torch, dev)
+        if h is not None:
+            ident["uuid"] = str(smi.amdsmi_get_gpu_device_uuid(h))
+            ident["smi_bdf"] = str(smi.amdsmi_get_gpu_device_bdf(h))
+    except Exception as e:  # noqa: BLE001 -- identity falls back to HIP's own fields
+        ident["smi_error"] = f"{type(e).__name__}: {e}"
+    finally:
+        if smi is not None:
+            try:
+                smi.amdsmi_shut_down()
+            except Exception:  # noqa: BLE001
+                pass
+    if ident["uuid"] is None and getattr(p, "uuid", None) is not None:
+        ident["uuid"] = str(p.uuid)
+    return ident
 
 
 def power_window(hasher, torch, dev, seconds):
@@ -329,6 +377,8 @@ def cpu_baseline(host_addr, n_chunks, gpu_digests, min_s=1.0, reps=3):
 
     def run(fn, nthreads, n):
         rates, passes = [], 0
+        # each leg's parity flag must reflect its own writes, not an earlier leg's
+        ctypes.memset(out, 0, ctypes.sizeof(out))
         for _ in range(reps):
             t0, k = time.perf_counter(), 0
             while True:
@@ -451,6 +501,27 @@ def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
     return out
 
 
+def find_traffic(want, path=None):
+    """(HBM bytes per launch, note) from the PMC traffic file measured on this
+    very build -- source id, kernel, variant and layout all equal to `want` --
+    else (None, why).  Default: the newest profiles/traffic_r*.json that
+    matches."""
+    paths = [path] if path else sorted(glob.glob(os.path.join(HERE, "profiles", "traffic_r*.json")), reverse=True)
+    tried = []
+    for p in paths:
+        rel = os.path.relpath(p, HERE)
+        try:
+            tj = json.load(open(p))
+        except (OSError, ValueError) as e:
+            tried.append(f"{rel}: unreadable ({e})")
+            continue
+        diff = {k: (tj.get(k), v) for k, v in want.items() if tj.get(k) != v}
+        if not diff:
+            return tj.get("hbm_bytes_per_launch"), f"{rel} (rocprofv3 --pmc, same source id)"
+        tried.append(f"{rel} was measured on another build/layout: {diff}")
+    return None, "; ".join(tried) or "no PMC traffic file for this build"
+
+
 # ---------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
@@ -472,7 +543,9 @@ def main():
     ap.add_argument("--backend", default="gloo",
                     help="process group for the control plane (barriers, timings, digest gather); "
                          "the hash path has no collective")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r03.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic file (default: the newest profiles/traffic_r*.json measured on this "
+                         "build's source id, kernel, variant and layout)")
     ap.add_argument("--digest-sample", type=int, default=3,
                     help="digests of this many chunks of EVERY rank (first, last, evenly between) in the line, "
                          "for parity checks beyond the golden range (0 = off)")
@@ -480,6 +553,15 @@ def main():
 
     import torch
     import torch.distributed as dist
+
+    phases = {}
+    t_phase = time.perf_counter()
+
+    def phase(name):
+        nonlocal t_phase
+        now = time.perf_counter()
+        phases[name] = round(now - t_phase, 2)
+        t_phase = now
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -496,15 +578,32 @@ def main():
     if rank == 0:
         ensure_built()
     shard.barrier(world, group)
+    variant = (args.ring, args.lines, args.nt) if args.ring else DEFAULT_VARIANT
+    if variant != DEFAULT_VARIANT and "BT_SHA1_LIB" not in os.environ:
+        # the rejected hot-kernel variants exist only in the experiments build
+        os.environ["BT_SHA1_LIB"] = os.path.join(HERE, "build_variants", "experiments", "libbtsha1.so")
     bt = _load("btsha1", os.path.join(PKG, "btsha1.py"))
     if args.ring:
-        bt.set_variant(args.ring, args.lines, args.nt)
+        bt.set_variant(*variant)
 
     C, pitch = args.chunks, args.pitch
-    first_chunk, _ = shard.weak_range(rank, C)
-    hasher = DeviceHasher(bt, torch, C, pitch, first_chunk)
-    res = shard.run_rank(hasher, args.steps, args.warmup, world, rank, group)
+    first_chunk, last_chunk = shard.weak_range(rank, C)
     kernel = bt.kernel_name(C)
+    # Which GPU each rank drives, before anything is allocated or timed: an
+    # N > 1 line must show N distinct devices (PCI address + UUID per rank).
+    ident = dict(rank=rank, **device_identity(torch, dev), kernel=kernel, chunk_range=[first_chunk, last_chunk])
+    idents = shard.gather_objects(ident, world, group)
+    clash = shard.check_distinct_devices(idents, world)
+    if clash:
+        print(f"bench.py rank {rank}: {clash}", file=sys.stderr, flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(3)
+    phase("init_s")
+    hasher = DeviceHasher(bt, torch, C, pitch, first_chunk)
+    phase("fill_s")
+    res = shard.run_rank(hasher, args.steps, args.warmup, world, rank, group)
+    phase("warmup_and_timed_s")
 
     clock = None
     if world == 1 and not args.no_clock and kernel == "k_sha1_fixed":
@@ -516,6 +615,7 @@ def main():
                                "timed region"}
         except Exception as e:  # noqa: BLE001 -- the clock evidence must never cost the bench line
             clock = {"error": f"{type(e).__name__}: {e}"}
+        phase("clock_s")
 
     # Every rank measures its own GPU's power (all ranks run the window together).
     power = None
@@ -531,6 +631,7 @@ def main():
             power = {"per_gpu": [dict(rank=r, **{k: (v if v >= 0 else None) for k, v in zip(keys, row)})
                                  for r, row in enumerate(allp)],
                      "method": power.get("method") if isinstance(power, dict) else None}
+        phase("power_s")
 
     line = None
     if rank == 0:
@@ -574,22 +675,10 @@ def main():
                 parity_all = table[str(world * C)] == digests_sha1
 
         # PMC traffic, only when measured on this very build and layout.
-        traffic, traffic_note = None, None
-        if os.path.exists(args.traffic_json):
-            try:
-                tj = json.load(open(args.traffic_json))
-                want = {"chunks": C, "pitch": pitch, "source_id": bt.source_id(), "kernel": kernel,
-                        "variant": bt.build_info().split("ring=")[1].split()[0]}
-                diff = {k: (tj.get(k), v) for k, v in want.items() if tj.get(k) != v}
-                if diff:
-                    traffic_note = f"{os.path.relpath(args.traffic_json, HERE)} was measured on another build/layout: {diff}"
-                else:
-                    traffic = tj.get("hbm_bytes_per_launch")
-                    traffic_note = f"{os.path.relpath(args.traffic_json, HERE)} (rocprofv3 --pmc, same source id)"
-            except (OSError, ValueError) as e:
-                traffic_note = f"unreadable: {e}"
-        else:
-            traffic_note = "no PMC traffic file for this build"
+        want = {"chunks": C, "pitch": pitch, "source_id": bt.source_id(), "kernel": kernel,
+                "variant": bt.build_info().split("ring=")[1].split()[0]}
+        traffic, traffic_note = find_traffic(want, args.traffic_json)
+        phase("gather_and_parity_s")
 
         extras_host = None
         if world == 1 and (not args.no_cpu_baseline or not args.no_host_path):
@@ -612,6 +701,7 @@ def main():
                 cpu = cpu_baseline(extras_host.ctypes.data, min(args.cpu_chunks, C), all_dig)
             except Exception as e:  # the checker must never cost the bench line
                 cpu = {"error": f"{type(e).__name__}: {e}"}
+            phase("cpu_baseline_s")
 
         verify = None
         if world == 1:
@@ -619,6 +709,7 @@ def main():
                 verify = hasher.verify_rate()
             except Exception as e:  # noqa: BLE001 -- never costs the bench line
                 verify = {"error": f"{type(e).__name__}: {e}"}
+            phase("verify_dev_s")
 
         host = None
         if world == 1 and not args.no_host_path and pitch == CHUNK:
@@ -627,6 +718,7 @@ def main():
                 host = host_paths(bt, torch, hasher.buf, extras_host[:n_img * CHUNK], all_dig[:20 * n_img])
             except Exception as e:
                 host = {"error": f"{type(e).__name__}: {e}"}
+            phase("host_path_s")
 
         peak_at_clock = (VALU_MIX_PEAK_TOPS * (clock["in_kernel_mhz"] / 1000.0 / CLOCK_GHZ)
                          if clock and "in_kernel_mhz" in clock else None)
@@ -669,8 +761,11 @@ def main():
                               "in-kernel clock (peak_at_measured_clock)"},
             "clock": clock,
             "power": power,
-            "per_gpu": [{"rank": r, "GiB_per_s": round(C * CHUNK * args.steps / w / 2**30, 3),
+            # per rank: its rate and kernel time, and which GPU it was (PCI address,
+            # UUID, devices visible), which kernel it ran and on which global chunks
+            "per_gpu": [{**idents[r], "GiB_per_s": round(C * CHUNK * args.steps / w / 2**30, 3),
                          "kernel_ms": round(k, 4)} for r, (w, k) in enumerate(res["per_rank"])],
+            "distinct_gpus": len({i["pci_bdf"] for i in idents}),
             "parity_first_4096_vs_golden": parity,
             "digest_sample": sample,
             "digests_sha1": digests_sha1,
@@ -678,6 +773,9 @@ def main():
             "cpu_baseline": cpu,
             "verify_dev": verify,
             "host_path": host,
+            "phases_s": phases,
+            # this process's age when the line is printed (interpreter start -> print)
+            "bench_wall_s": process_age_s(),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

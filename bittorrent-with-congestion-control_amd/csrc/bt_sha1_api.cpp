@@ -868,7 +868,12 @@ int bt_sha1_debug_barrier_stats(uint64_t out[3], int reset) {
 int bt_sha1_set_variant(int nbuf, int lines, int nt) {
   const int code = nbuf * 100 + lines * 10 + (nt ? 1 : 0);
   if (!btsha1_fixed_variant_ok(code)) {
-    set_err("no hot-kernel variant ring=%d lines=%d nt=%d", nbuf, lines, nt);
+    if (btsha1_experiments_build())
+      set_err("no hot-kernel variant ring=%d lines=%d nt=%d", nbuf, lines, nt);
+    else
+      set_err("no hot-kernel variant ring=%d lines=%d nt=%d in the product library: it carries only the default "
+              "(3, 1, 0); the rejected variants are in build_variants/experiments/libbtsha1.so (make experiments)",
+              nbuf, lines, nt);
     return -1;
   }
   g_variant.store(code);

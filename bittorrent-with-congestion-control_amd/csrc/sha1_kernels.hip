@@ -15,7 +15,8 @@
 //                   descriptor: per-lane 32-bit voffset = lane * pitch, the
 //                   line offset rides in the scalar soffset -> zero VALU
 //                   address arithmetic in the loop.
-//   k_sha1_lds      the hot path with coalesced LDS-DMA staging (a variant).
+//   k_sha1_lds      the hot path with coalesced LDS-DMA staging (a rejected
+//                   variant: built only into the experiments library).
 //   k_sha1_lat      small fixed-layout batches (<= 128 chunks per CU, 32768 on
 //                   MI355X: small verify batches): a loader/schedule wave and a round
 //                   wave per 64 chunks meet in LDS, cutting a lone chain's
@@ -1196,22 +1197,27 @@ uint64_t btsha1_latency_batch() {
   return v == BT_SHA1_LATENCY_AUTO ? (uint64_t)btsha1_device_cus() * 128u : v;
 }
 
+// Variant code: NBUF*100 + L*10 + (nt ? 1 : 0).  The product library carries
+// ONE hot kernel, the measured default (3-slot ring of one 128-byte line,
+// plain loads).  The rejected variants -- other ring shapes,
+// non-temporal loads, the LDS-staged kernel -- exist only in the experiments
+// library (make experiments: -DBT_SHA1_EXPERIMENTS), where bt_sha1_set_variant
+// selects among them; the product's bt_sha1_set_variant accepts only 310.
+#ifdef BT_SHA1_EXPERIMENTS
 constexpr int kLdsVariant = 1010;  // bt_sha1_set_variant(10, 1, 0): LDS-staged k_sha1_lds
 constexpr int kLdsNtVariant = 1011;  // bt_sha1_set_variant(10, 1, 1): the same with nt DMA loads
-
-// Variant code: NBUF*100 + L*10 + (nt ? 1 : 0).  The diagnostic builds
-// (make asan / dbgbar: -DBT_SHA1_ONE_VARIANT) carry only the default variant:
-// each hot-kernel instantiation is ~45 KB of code, and those libraries travel
-// with every GPU lease.
-#ifdef BT_SHA1_ONE_VARIANT
-#define BT_FIXED_VARIANTS(X) X(3, 1, 0)
-#else
 #define BT_FIXED_VARIANTS(X) X(2, 1, 0) X(3, 1, 0) X(4, 1, 0) X(2, 2, 0) \
   X(2, 1, 2) X(3, 1, 2) X(2, 2, 2)
+bool btsha1_experiments_build() { return true; }
+#else
+#define BT_FIXED_VARIANTS(X) X(3, 1, 0)
+bool btsha1_experiments_build() { return false; }
 #endif
 
 bool btsha1_fixed_variant_ok(int code) {
+#ifdef BT_SHA1_EXPERIMENTS
   if (code == kLdsVariant || code == kLdsNtVariant) return true;
+#endif
 #define BT_CASE(N, L, A) if (code == N * 100 + L * 10 + (A ? 1 : 0)) return true;
   BT_FIXED_VARIANTS(BT_CASE)
 #undef BT_CASE
@@ -1228,6 +1234,7 @@ hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uin
   if (total <= btsha1_chain_batch() && total <= btsha1_latency_batch())
     return btsha1_launch_chain(d_in, nullptr, nullptr, pitch, len, n, d_dig, s, tail_len, d_exp, d_ok);
   if (total <= btsha1_latency_batch()) return launch_lat(d_in, n, pitch, len, d_dig, d_exp, d_ok, s, tail_len);
+#ifdef BT_SHA1_EXPERIMENTS
   if (variant == kLdsVariant || variant == kLdsNtVariant) {
     if (n) {
       const hipError_t e = variant == kLdsVariant ? launch_lds<0>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s)
@@ -1239,6 +1246,7 @@ hipError_t btsha1_launch_fixed(const void *d_in, uint64_t n, uint32_t pitch, uin
                                            d_dig ? d_dig + 20 * n : nullptr, s)
                     : hipSuccess;
   }
+#endif
 #define BT_CASE(N, L, A) \
   if (variant == N * 100 + L * 10 + (A ? 1 : 0)) \
     return launch_fixed_v<N, L, A>(d_in, n, pitch, len, d_dig, d_exp, d_ok, s, tail_len);
@@ -1263,7 +1271,11 @@ const char *btsha1_fixed_kernel_name(uint64_t n, int variant) {
   if (n == 0) return "none";
   if (n <= btsha1_chain_batch() && n <= btsha1_latency_batch()) return "k_sha1_chain";
   if (n <= btsha1_latency_batch()) return "k_sha1_lat";
+#ifdef BT_SHA1_EXPERIMENTS
   if (variant == kLdsVariant || variant == kLdsNtVariant) return "k_sha1_lds";
+#else
+  (void)variant;
+#endif
   return "k_sha1_fixed";
 }
 

@@ -36,7 +36,10 @@ uint64_t btsha1_chain_batch();
 // Compute units of the current device (cached per device; 256 on MI355X).
 uint32_t btsha1_device_cus();
 // Hot-kernel variant code = ring slots*100 + lines per slot*10 + nt flag.
+// The product build knows only 310; the experiments build
+// (-DBT_SHA1_EXPERIMENTS) also the rejected ring / nt / LDS-staged variants.
 bool btsha1_fixed_variant_ok(int code);
+bool btsha1_experiments_build();
 // n messages at d_base + d_off[i], d_len[i] bytes each; with d_off == NULL,
 // message i is at d_base + i*pitch, fixed_len bytes.  Any alignment.  At most
 // btsha1_chain_batch() messages take the chain kernel, more the one-message-

@@ -57,6 +57,38 @@ def gather_floats(values, world, group=None):
     return [[float(x) for x in p] for p in parts]
 
 
+def gather_objects(obj, world, group=None):
+    """Every rank's (picklable, small) object, in rank order, on every rank."""
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
+def check_distinct_devices(idents, world):
+    """The N > 1 line must come from N distinct GPUs.  `idents` is every
+    rank's {"rank", "pci_bdf", "device_count", ...}.  When each rank can see at
+    least `world` devices (a full node: rank r drives device r), two ranks on
+    one PCI address is a launch error -> the message; otherwise None.  With
+    fewer visible devices than ranks (the one-GPU rehearsal, or one device per
+    rank through *_VISIBLE_DEVICES) ranks may share a device by design and
+    the guard stays off; the line still records every rank's address."""
+    if world <= 1 or len(idents) != world:
+        return None
+    if min(int(i.get("device_count") or 0) for i in idents) < world:
+        return None
+    seen = {}
+    for i in idents:
+        seen.setdefault(i.get("pci_bdf"), []).append(i.get("rank"))
+    dup = {bdf: ranks for bdf, ranks in seen.items() if len(ranks) > 1}
+    if dup:
+        return (f"{world} ranks see >= {world} devices each, but ranks share a GPU: "
+                + ", ".join(f"{bdf} <- ranks {ranks}" for bdf, ranks in sorted(dup.items(), key=str)))
+    return None
+
+
 def gather_digests(local: bytes, world, rank, group=None):
     """Host-side gather of per-rank digest slices to rank 0, in rank order
     (== global chunk order for both splits above).  Returns the concatenation

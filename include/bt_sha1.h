@@ -130,7 +130,11 @@ int bt_sha1_host_unregister(void *h_ptr);
  * lanes, grown on demand and reused by later calls -- up to 2 x 1 GiB of
  * page-locked host memory (pageable input) and 2 x 1 GiB of HBM.  Pinned or
  * registered input is DMA'd in bigger batches (BT_SHA1_DMA_BATCH_MB, 4 GiB
- * by default); those HBM batches are freed before the call returns. */
+ * by default); those HBM batches are freed before the call returns.  Freeing
+ * them (hipFree) synchronises the whole device: such a call returns only
+ * after work other streams of this process queued on the GPU has finished,
+ * and callers that share the GPU with latency-sensitive streams should hash
+ * pinned input in pieces of <= 2 GiB (kept lanes, no free) or use staging. */
 int64_t bt_sha1_chunks_host(const void *h_in, uint64_t total_len, uint64_t chunk_len,
                             uint8_t *h_digests);
 /* The same split over the first `ndev` GPUs (<=0: all), one host thread per

@@ -2,13 +2,18 @@
  * oracle/oracle_selftest.c -- TEST ONLY.  Drives the oracle restatement under
  * -fsanitize=address,undefined (oracle/Makefile target oracle_asan): the NIST
  * KATs of sha.c:32-38, chunk.c's "dash" round trip, every split point of the
- * byte-buffered update around block boundaries, and the pthread batch driver.
+ * byte-buffered update around block boundaries, and the pthread batch driver
+ * (incl. threads that cannot be created: a clean -1, never a join of an
+ * unset pthread_t).
  * Exit status 0 = all checks passed.
  */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 typedef struct {
   uint64_t bits;
@@ -105,6 +110,24 @@ int main(void) {
   }
   if (or_synth_digests(0, 1, 12, 77, c2, 1) != -1) {
     puts("FAIL synth digests accepted a chunk length that is not a multiple of 8");
+    fails++;
+  }
+  /* thread creation refused (RLIMIT_NPROC in a child, as an unprivileged
+   * user): both batch drivers return -1 after joining only the threads that
+   * started, instead of joining unset handles or reporting partial output. */
+  fflush(stdout);
+  pid_t pid = fork();
+  if (pid == 0) {
+    if (geteuid() == 0 && (setgid(65534) || setuid(65534))) _exit(3);
+    struct rlimit one = {1, 1};
+    if (setrlimit(RLIMIT_NPROC, &one)) _exit(4);
+    const int rh = or_hash_chunks(img, n, L, L, 999, b, 8);
+    const int rs = or_synth_digests(first, m, L, 77, c2, 8);
+    _exit(rh == -1 && rs == -1 ? 0 : 5);
+  }
+  int st = 0;
+  if (pid < 0 || waitpid(pid, &st, 0) != pid || !WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+    printf("FAIL thread-creation failure not reported cleanly (status %d)\n", st);
     fails++;
   }
   free(img2);

@@ -89,7 +89,8 @@ def hash_chunks(data, chunk_len, pitch=None, nthreads=1, lib=None):
         src = (ctypes.c_uint8 * len(data)).from_buffer(data)
     else:
         src = _buf(data)
-    _lib.or_hash_chunks(src, n, pitch, chunk_len, last, out, nthreads)
+    if _lib.or_hash_chunks(src, n, pitch, chunk_len, last, out, nthreads):
+        raise RuntimeError("or_hash_chunks failed (out of memory, or a worker thread could not be created)")
     raw = bytes(out)
     return [raw[20 * i:20 * i + 20] for i in range(n)]
 
@@ -114,7 +115,8 @@ def synth_digests(first_chunk, n, chunk_len=CHUNK, seed=SEED_SYNTH, nthreads=Non
     batch in seconds, with no image in memory."""
     out = (ctypes.c_uint8 * max(20 * n, 1))()
     if _lib.or_synth_digests(first_chunk, n, chunk_len, seed, out, nthreads or usable_cpus()):
-        raise ValueError("or_synth_digests failed (chunk_len must be a multiple of 8)")
+        raise ValueError("or_synth_digests failed (chunk_len must be a multiple of 8; or out of memory, "
+                         "or a worker thread could not be created)")
     return bytes(out)[:20 * n]
 
 

@@ -213,26 +213,45 @@ static void *or_worker(void *arg) {
   return NULL;
 }
 
+/* Run worker(jobs[t]) for t < nthreads: job 0 on the calling thread, the
+ * others on pthreads.  A thread that fails to start is never joined (its
+ * pthread_t is unset); the call then returns -1 after joining the threads
+ * that did start, so the caller reports a clean failure instead of reading a
+ * partly written output. */
+static int or_run_jobs(void *(*worker)(void *), void *jobs, size_t job_size, int nthreads) {
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  unsigned char *started = (unsigned char *)calloc((size_t)nthreads, 1);
+  if (!th || !started) {
+    free(th);
+    free(started);
+    return -1;
+  }
+  int failed = 0;
+  for (int t = 1; t < nthreads; t++) {
+    if (pthread_create(&th[t], NULL, worker, (char *)jobs + (size_t)t * job_size) == 0)
+      started[t] = 1;
+    else
+      failed = 1;
+  }
+  worker(jobs);
+  for (int t = 1; t < nthreads; t++)
+    if (started[t]) pthread_join(th[t], NULL);
+  free(th);
+  free(started);
+  return failed ? -1 : 0;
+}
+
 int or_hash_chunks(const uint8_t *base, uint64_t n, uint64_t pitch, uint32_t chunk_len,
                    uint32_t last_len, uint8_t *out, int nthreads) {
   if (nthreads < 1) nthreads = 1;
   if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
-  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
   or_job *jobs = (or_job *)calloc((size_t)nthreads, sizeof(or_job));
-  if (!th || !jobs) {
-    free(th);
-    free(jobs);
-    return -1;
-  }
-  for (int t = 0; t < nthreads; t++) {
+  if (!jobs) return -1;
+  for (int t = 0; t < nthreads; t++)
     jobs[t] = (or_job){base, pitch, n * t / nthreads, n * (t + 1) / nthreads, n, chunk_len, last_len, out};
-    if (t) pthread_create(&th[t], NULL, or_worker, &jobs[t]);
-  }
-  or_worker(&jobs[0]);
-  for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
-  free(th);
+  const int rc = or_run_jobs(or_worker, jobs, sizeof(or_job), nthreads);
   free(jobs);
-  return 0;
+  return rc;
 }
 
 /* ---- digests of synthetic chunks, regenerated on the fly ---------------------
@@ -267,24 +286,12 @@ int or_synth_digests(uint64_t first_chunk, uint64_t n, uint32_t chunk_len, uint6
   if (chunk_len % 8) return -1;
   if (nthreads < 1) nthreads = 1;
   if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
-  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
   or_synth_job *jobs = (or_synth_job *)calloc((size_t)nthreads, sizeof(or_synth_job));
-  if (!th || !jobs) {
-    free(th);
-    free(jobs);
-    return -1;
-  }
-  for (int t = 0; t < nthreads; t++) {
+  if (!jobs) return -1;
+  for (int t = 0; t < nthreads; t++)
     jobs[t] = (or_synth_job){first_chunk, n * t / nthreads, n * (t + 1) / nthreads, seed, chunk_len, out, 0};
-    if (t) pthread_create(&th[t], NULL, or_synth_worker, &jobs[t]);
-  }
-  or_synth_worker(&jobs[0]);
-  int err = jobs[0].err;
-  for (int t = 1; t < nthreads; t++) {
-    pthread_join(th[t], NULL);
-    err |= jobs[t].err;
-  }
-  free(th);
+  int err = or_run_jobs(or_synth_worker, jobs, sizeof(or_synth_job), nthreads);
+  for (int t = 0; t < nthreads; t++) err |= jobs[t].err;  /* jobs that never started keep err = 0 */
   free(jobs);
   return err ? -1 : 0;
 }

@@ -91,6 +91,49 @@ def test_barrier_tallies_only_in_the_debug_build():
     assert b"g_bar_stats" not in open(LIB, "rb").read()
 
 
+EXP_LIB = os.path.join(REPO, "build_variants", "experiments", "libbtsha1.so")
+
+
+def _kernel_symbols(lib):
+    """Mangled kernel names in a library's gfx950 code object."""
+    blob = open(lib, "rb").read()
+    return set(m.decode() for m in re.findall(rb"_ZN6btsha1\d+k_sha1_\w+?(?=\x00|\.kd)", blob))
+
+
+def test_product_library_carries_only_the_default_hot_kernel():
+    """One compression, one hot path in the product (sha.c:176-451): the
+    rejected ring / nt / LDS-staged variants live only in the experiments
+    library, and the product's bt_sha1_set_variant refuses them (no device
+    call is made, so this runs without a GPU)."""
+    bt = load_btsha1()
+    for v in ((4, 1, 0), (2, 1, 0), (2, 2, 0), (3, 1, 1), (10, 1, 0), (10, 1, 1)):
+        with pytest.raises(bt.BtSha1Error, match="experiments"):
+            bt.set_variant(*v)
+    bt.set_variant(3, 1, 0)  # the default stays selectable
+    prod = _kernel_symbols(LIB)
+    fixed = {s for s in prod if "k_sha1_fixed" in s}
+    assert fixed and all("ILi3ELi1ELi0E" in s for s in fixed), fixed
+    assert not any("k_sha1_lds" in s for s in prod), prod
+    assert os.path.exists(EXP_LIB), "run make experiments first"
+    exp = _kernel_symbols(EXP_LIB)
+    assert any("k_sha1_lds" in s for s in exp) and any("ILi4ELi1ELi0E" in s for s in exp)
+    assert os.path.getsize(LIB) < 0.5 * os.path.getsize(EXP_LIB)
+
+
+def test_diagnostic_builds_carry_their_own_source_id():
+    """bench.py reuses PMC traffic only for the source id it was measured on:
+    every diagnostic / experiment build reports a suffixed id."""
+    prod = subprocess.run([sys.executable, "-c", "import ctypes,sys; l=ctypes.CDLL(sys.argv[1]); "
+                           "l.bt_sha1_source_id.restype=ctypes.c_char_p; print(l.bt_sha1_source_id().decode())", LIB],
+                          capture_output=True, text=True, check=True).stdout.strip()
+    for name, suffix in (("experiments", "-exp"), ("dbgbar", "-dbgbar")):
+        lib = os.path.join(REPO, "build_variants", name, "libbtsha1.so")
+        out = subprocess.run([sys.executable, "-c", "import ctypes,sys; l=ctypes.CDLL(sys.argv[1]); "
+                              "l.bt_sha1_source_id.restype=ctypes.c_char_p; print(l.bt_sha1_source_id().decode())",
+                              lib], capture_output=True, text=True, check=True).stdout.strip()
+        assert out == prod + suffix, (name, out, prod)
+
+
 def test_sha1context_layout_matches_reference():
     bt = load_btsha1()
     # sha.h:39-50 of the reference: u64 + 5*u32 + u32 + 64-byte union = 96 bytes
@@ -120,7 +163,9 @@ def test_reference_callers_compile_and_link_against_dropin(tmp_path):
 
 def test_integration_peer_example_compiles(tmp_path):
     """The batched-verify snippet of INTEGRATION.md §3 compiles and links against
-    include/ + libbtsha1.so as written (guards the documented calls against drift)."""
+    include/ + libbtsha1.so as written, over the reference's own Chunk /
+    Request layout (guards the documented calls against drift); its per-chunk
+    table is sized from the request, never a fixed array indexed by chunk id."""
     import re
     text = open(os.path.join(REPO, "INTEGRATION.md")).read()
     sec = text[text.index("## 3."):]
@@ -128,13 +173,15 @@ def test_integration_peer_example_compiles(tmp_path):
     body = "\n".join(l for l in body.splitlines() if not l.startswith("#include"))
     src = tmp_path / "peer_example.c"
     src.write_text(
-        "#include <stdint.h>\n#include \"bt_sha1.h\"\n#include \"chunk.h\"\n"
+        "#include <stdint.h>\n#include <stdlib.h>\n#include \"bt_sha1.h\"\n#include \"chunk.h\"\n"
         "enum { NOT_STARTED, RECEIVING, VERIFYING, OWNED };\n"
-        "struct Chunk { int state; char *data; uint32_t received_byte_number; uint8_t hash[20]; };\n"
-        "struct Request { struct Chunk chunks[4]; };\n"
+        "struct Chunk { int id; uint8_t hash[20]; int state; char *data; int received_seq_number;\n"
+        "               int received_byte_number; };\n"          # common.h:45-52
+        "struct Request { char *filename; int chunk_number; struct Chunk *chunks; };\n"  # common.h:54-58
         "void peer_example(struct Chunk *chunk, int chunk_id, struct Request *current_request) {\n"
         + body + "\n}\nint main(void) { return 0; }\n")
     exe = tmp_path / "peer_example"
+    assert "calloc((size_t)current_request->chunk_number" in body and not re.search(r"static[^;]*\[\d+\];", body)
     r = subprocess.run(["gcc", "-Wall", "-Wno-unused-variable", "-Werror", "-I", os.path.join(REPO, "include"),
                         "-o", str(exe), str(src), f"-L{PKG}", "-lbtsha1", f"-Wl,-rpath,{PKG}"],
                        capture_output=True, text=True)

@@ -55,6 +55,24 @@ def _run_bench(world, chunks, *extra, timeout=240):
     return json.loads(lines[0])
 
 
+def _check_identity(line, world, chunks):
+    """Every per_gpu entry says which GPU the rank drove (PCI address, UUID,
+    devices visible), which kernel it ran and on which global chunks.  All
+    ranks share this box's one GPU, so the addresses are equal and the
+    distinct-device guard stays off (device_count 1 < world)."""
+    per = line["per_gpu"]
+    assert [p["rank"] for p in per] == list(range(world))
+    for r, p in enumerate(per):
+        for k in ("pci_bdf", "uuid", "device_count", "hip_device", "kernel", "chunk_range"):
+            assert k in p, (k, p)
+        assert p["kernel"] == line["roofline"]["kernel"]
+        assert p["chunk_range"] == [r * chunks, (r + 1) * chunks]
+        assert p["device_count"] >= 1 and len(p["pci_bdf"].split(":")) == 3
+    assert len({p["pci_bdf"] for p in per}) == line["distinct_gpus"]
+    if per[0]["device_count"] < world:
+        assert line["distinct_gpus"] == 1 and len({p["uuid"] for p in per}) == 1
+
+
 def _check_sample(line, world, chunks, oracle):
     """Every rank's sampled digests == the oracle on the regenerated chunk."""
     sample = line["digest_sample"]
@@ -88,6 +106,7 @@ def test_bench_ranks_split_and_gather_on_one_gpu(world, oracle):
     assert line["cpu_baseline"] is None and line["host_path"] is None
     # every rank read its own GPU's board power after the timed region
     assert [p["rank"] for p in line["power"]["per_gpu"]] == list(range(world))
+    _check_identity(line, world, chunks)
     _check_sample(line, world, chunks, oracle)
 
 
@@ -103,6 +122,7 @@ def test_bench_ranks_run_the_hot_kernel_with_parity_on_every_rank(oracle, chunks
     assert line["config"]["global_chunks"] == world * chunks
     assert line["parity_first_4096_vs_golden"] is True   # rank 0's first 4096 vs sha.c golden
     assert [p["rank"] for p in line["per_gpu"]] == [0, 1]
+    _check_identity(line, world, chunks)
     _check_sample(line, world, chunks, oracle)
 
 
@@ -121,6 +141,8 @@ def test_bench_single_rank_line_checks(oracle):
     line = json.loads(lines[0])
     assert line["n_gpus"] == 1 and line["parity_first_4096_vs_golden"] is True
     assert line["parity_all_vs_golden"] is True
+    _check_identity(line, 1, 4096)
+    assert 0 < line["bench_wall_s"] < 600 and line["phases_s"]["warmup_and_timed_s"] > 0
     v = line["verify_dev"]
     assert v["flags_correct"] is True and v["mismatches_planted"] == len(range(0, 4096, 997)) and v["GiB_per_s"] > 0
     _check_sample(line, 1, 4096, oracle)

@@ -158,15 +158,16 @@ def synth4096(bt, torch, oracle):
     return buf
 
 
-LDS = 10  # bt_sha1_set_ring_depth(10): the LDS-staged hot kernel (k_sha1_lds)
 LAT = "lat"  # bt_sha1_set_latency_batch: the two-wave latency kernel (k_sha1_lat)
 CHAIN = "chain"  # bt_sha1_set_chain_batch: one two-wave workgroup per chunk (k_sha1_chain)
 
 
 @contextlib.contextmanager
 def kernel_mode(bt, mode):
-    """Pin the fixed-layout launches to one kernel: LAT, CHAIN, a ring depth or
-    a (nbuf, lines, nt) variant (latency and chain kernels off).  Restores the
+    """Pin the fixed-layout launches to one kernel: LAT, CHAIN, or the hot
+    kernel (3 = its ring depth; latency and chain kernels off).  The product
+    library has no other hot-kernel variant (the rejected ones are checked in
+    tests/test_gpu_variants.py against the experiments build).  Restores the
     defaults."""
     prev = bt.set_latency_batch(1 << 62 if mode in (LAT, CHAIN) else 0)
     prev_chain = bt.set_chain_batch(1 << 62 if mode == CHAIN else 0)
@@ -180,12 +181,11 @@ def kernel_mode(bt, mode):
         bt.set_chain_batch(prev_chain)
 
 
-@pytest.mark.parametrize("variant", [(2, 1, 0), (3, 1, 0), (4, 1, 0), (2, 2, 0), (3, 1, 1), (LDS, 1, 0), (LDS, 1, 1),
-                                     LAT, CHAIN])
+@pytest.mark.parametrize("variant", [(3, 1, 0), LAT, CHAIN])
 def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, variant):
     """BASELINE config 2: 4096 synthetic 512 KiB chunks, every digest == sha.c's,
-    for every compiled hot-kernel variant (ring depth, slot lines, nt, LDS-staged)
-    and the latency kernel."""
+    through each kernel of the product library a fixed-layout batch can run:
+    the hot kernel, the latency kernel and the chain kernel."""
     with kernel_mode(bt, variant):
         n = 4096
         out = torch.zeros(20 * n, dtype=torch.uint8, device="cuda")
@@ -196,7 +196,7 @@ def test_config2_4096_chunks_bit_exact(bt, torch, synth4096, variant):
         assert got == read_pairs("synth4096.txt")
 
 
-@pytest.mark.parametrize("ring", [3, LDS, LAT, CHAIN])
+@pytest.mark.parametrize("ring", [3, LAT, CHAIN])
 def test_verify_dev_flags_mismatches(bt, torch, synth4096, ring):
     with kernel_mode(bt, ring):
         _verify_dev_flags_mismatches(bt, torch, synth4096)
@@ -227,7 +227,7 @@ def _verify_dev_flags_mismatches(bt, torch, synth4096):
     (1000, 1003, 67),            # odd pitch -> generic kernel
     (CHUNK, CHUNK + 256, 65),    # padded pitch, fast kernel
 ])
-@pytest.mark.parametrize("ring", [3, LDS, LAT, CHAIN])
+@pytest.mark.parametrize("ring", [3, LAT, CHAIN])
 def test_fixed_layouts_vs_oracle(bt, torch, oracle, chunk_len, pitch, n, ring):
     total = pitch * (n - 1) + chunk_len
     host = bytearray(oracle.fill_synthetic(total, 11, 0xC0FFEE))
@@ -241,7 +241,7 @@ def test_fixed_layouts_vs_oracle(bt, torch, oracle, chunk_len, pitch, n, ring):
 
 
 def _ragged_line_counts(bt, torch, oracle, ring):
-    deepest = 4 if ring in (LDS, LAT, CHAIN) else ring
+    deepest = 4 if ring in (LAT, CHAIN) else ring
     for blocks in range(0, 2 * 2 * deepest + 3):
         for r in (0, 5, 56):
             L = 64 * blocks + r
@@ -257,8 +257,8 @@ def _ragged_line_counts(bt, torch, oracle, ring):
                 assert got[i] == oracle.sha1(bytes(host[i * pitch:i * pitch + L])), (ring, L, i)
 
 
-def test_every_ring_depth_on_ragged_line_counts(bt, torch, oracle):
-    for ring in (2, 3, 4, LDS, LAT, CHAIN):
+def test_every_kernel_on_ragged_line_counts(bt, torch, oracle):
+    for ring in (3, LAT, CHAIN):
         with kernel_mode(bt, ring):
             _ragged_line_counts(bt, torch, oracle, ring)
 
@@ -278,11 +278,10 @@ def test_host_pipeline_c_tar_and_tail(bt, oracle):
     assert bt.chunks_host(big, chunk_len=4096) == oracle.hash_chunks(big, 4096)
 
 
-@pytest.mark.parametrize("variant", [(3, 1, 0), (2, 2, 0), (LDS, 1, 0), LAT, CHAIN])
+@pytest.mark.parametrize("variant", [(3, 1, 0), LAT, CHAIN])
 def test_image_tail_in_same_launch(bt, oracle, variant):
     """launch_image: the short last chunk rides in the hot kernel's (or the
-    latency kernel's) tail wave; the LDS-staged variant hands it to the ragged
-    kernel instead."""
+    latency kernel's) tail wave."""
     with kernel_mode(bt, variant):
         for chunk_len in (4096, 64 * 1024):
             for nfull in (0, 1, 63, 64, 65, 130):
@@ -517,6 +516,41 @@ def test_registered_host_image_direct_dma(bt, oracle):
     try:
         assert bt.chunks_host_addr(addr, data.nbytes) == want      # pinned: direct DMA
         assert bt.chunks_host_addr(addr, data.nbytes, ndev=0) == want
+    finally:
+        bt.host_unregister(addr)
+
+
+def test_host_calls_give_their_hbm_back(bt, torch, oracle):
+    """HBM a host call holds beyond the device context's kept staging lanes
+    (2 x <= 1 GiB, include/bt_sha1.h) is freed before it returns: the
+    direct-DMA batches of a registered image (2 GiB per lane here) and the
+    worker contexts of repeated device ids (devs=[0,0,0]), registered and
+    pageable.  hipMemGetInfo after each call against the level after a first
+    pageable call that sized the kept lanes."""
+    import numpy as np
+    n = 8192  # 4 GiB: two direct-DMA batches of 2 GiB, two staged lanes of 1 GiB
+    img = np.empty(n * CHUNK, dtype=np.uint8)
+    words = img.view(np.uint64)
+    words[:] = np.arange(words.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    addr = img.ctypes.data
+    want = bt.chunks_host_addr(addr, img.nbytes)                 # pageable: sizes the kept lanes
+    for i in (0, 4097, n - 1):
+        assert want[20 * i:20 * i + 20] == oracle.sha1(img[i * CHUNK:(i + 1) * CHUNK].tobytes()), i
+    torch.cuda.synchronize()
+    kept = torch.cuda.mem_get_info()[0]
+    slack = 64 << 20
+
+    def free_now():
+        torch.cuda.synchronize()
+        return torch.cuda.mem_get_info()[0]
+    assert bt.chunks_host_addr(addr, img.nbytes, devs=[0, 0, 0]) == want    # pageable, 3 workers
+    assert free_now() >= kept - slack
+    bt.host_register(addr, img.nbytes)
+    try:
+        assert bt.chunks_host_addr(addr, img.nbytes) == want                 # direct DMA, 2 GiB batches
+        assert free_now() >= kept - slack
+        assert bt.chunks_host_addr(addr, img.nbytes, devs=[0, 0, 0]) == want  # registered, 3 workers
+        assert free_now() >= kept - slack
     finally:
         bt.host_unregister(addr)
 

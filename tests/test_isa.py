@@ -27,10 +27,47 @@ def asm(tmp_path_factory):
     return mod, open(out).read()
 
 
-@pytest.mark.parametrize("nbuf,lines", [(3, 1), (2, 1), (4, 1), (2, 2)])
-def test_hot_loop_mix(asm, nbuf, lines):
+@pytest.fixture(scope="module")
+def asm_exp(tmp_path_factory):
+    """The experiments library's kernels (rejected ring shapes, nt, LDS)."""
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("hipcc absent")
+    mod = _isa_mix()
+    out = str(tmp_path_factory.mktemp("isa_exp") / "k.s")
+    mod.compile_asm(out, experiments=True)
+    return mod, open(out).read()
+
+
+def test_hot_loop_mix(asm):
     mod, text = asm
-    m = mod.loop_mix(text, nbuf, lines)
+    _check_mix(mod.loop_mix(text, 3, 1))
+
+
+@pytest.mark.parametrize("nbuf,lines", [(3, 1), (2, 1), (4, 1), (2, 2)])
+def test_hot_loop_mix_experiment_variants(asm_exp, nbuf, lines):
+    """Every ring shape of the experiments build compresses with the same
+    597-instruction block (DESIGN.md §5 compares them at equal work)."""
+    mod, text = asm_exp
+    _check_mix(mod.loop_mix(text, nbuf, lines))
+
+
+def test_product_hot_kernel_is_the_experiments_default(asm, asm_exp):
+    """The product's k_sha1_fixed<3,1,...> is instruction for instruction the
+    experiments build's, so measurements of either apply to both."""
+    import re
+    mod, text = asm
+    _, etext = asm_exp
+
+    def body(t, sym):
+        b = t[t.index(sym + ":"):]
+        b = b[:b.index(".Lfunc_end")]
+        return [re.sub(r"BB\d+_", "BB_", l.split(";")[0].strip()) for l in b.splitlines() if l.split(";")[0].strip()]
+    sym = mod.fixed_symbol(3, 1)
+    assert body(text, sym) == body(etext, sym)
+    assert "k_sha1_lds" not in text and mod.fixed_symbol(4, 1) not in text
+
+
+def _check_mix(m):
     assert m["valu_per_block"] == 597, m
     assert m["half_rate_per_block"] == 400 and m["full_rate_per_block"] == 197, m
     assert m["mix_per_block"]["v_xor_b32_e32"] == 48 and m["mix_per_block"]["v_alignbit_b32"] == 224, m

@@ -119,6 +119,63 @@ def test_bench_rank_protocol_two_ranks(oracle):
     assert nranks == 2 and abs(kmax - 1.006) < 1e-9
 
 
+def _ident_worker(rank, world, port, shared, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shard = _load_shard()
+    bdf = "0000:05:00.0" if shared else f"0000:{0x05 + 0x10 * rank:02x}:00.0"
+    ident = {"rank": rank, "pci_bdf": bdf, "uuid": f"stub-{rank}", "device_count": world,
+             "kernel": "k_sha1_fixed", "chunk_range": list(shard.weak_range(rank, 131072))}
+    idents = shard.gather_objects(ident, world)
+    q.put((rank, idents, shard.check_distinct_devices(idents, world)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_rank_identities_gathered_and_shared_gpu_refused(shared):
+    """bench.py's pre-timing identity exchange at world size 2 (gloo): every
+    rank gets every rank's {PCI address, UUID, devices visible, kernel, chunk
+    range} in rank order, and when each rank sees >= world devices yet two
+    ranks report one PCI address, EVERY rank gets the clash (so all exit
+    before the timed region); stub identities stand in for the GPUs."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ident_worker, args=(r, world, port, shared, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, idents, clash in got:
+        assert [i["rank"] for i in idents] == [0, 1]
+        assert [i["chunk_range"] for i in idents] == [[0, 131072], [131072, 262144]]
+        if shared:
+            assert clash and "0000:05:00.0 <- ranks [0, 1]" in clash
+        else:
+            assert clash is None
+
+
+def test_distinct_device_guard_logic():
+    shard = _load_shard()
+
+    def ids(bdfs, count):
+        return [{"rank": r, "pci_bdf": b, "device_count": count} for r, b in enumerate(bdfs)]
+    full = [f"0000:{b:02x}:00.0" for b in (0x05, 0x15, 0x65, 0x75, 0x85, 0x95, 0xe5, 0xf5)]
+    assert shard.check_distinct_devices(ids(full, 8), 8) is None            # a full node, one GPU per rank
+    bad = full[:7] + [full[3]]
+    msg = shard.check_distinct_devices(ids(bad, 8), 8)
+    assert msg and "ranks [3, 7]" in msg                                     # two ranks on one GPU
+    assert shard.check_distinct_devices(ids([full[0]] * 8, 1), 8) is None   # one-GPU rehearsal: guard off
+    assert shard.check_distinct_devices(ids([full[0]] * 2, 1), 2) is None
+    assert shard.check_distinct_devices(ids(full[:4], 4), 8) is None        # incomplete gather: no verdict
+    assert shard.check_distinct_devices(ids(full[:1], 8), 1) is None        # N = 1
+
+
 def test_bench_uses_the_shard_protocol():
     """The bench's rank split / timing / gather is shard.py's (covered above),
     not an inline copy."""

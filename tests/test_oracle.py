@@ -186,3 +186,33 @@ def test_oracle_under_asan_ubsan(tmp_path):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0")
     r = subprocess.run([str(exe)], capture_output=True, text=True, env=env)
     assert r.returncode == 0 and "ok (0 failures)" in r.stdout, r.stdout + r.stderr
+
+
+def test_batch_drivers_report_refused_threads_cleanly():
+    """or_hash_chunks / or_synth_digests (the parity checker's threaded sweeps)
+    with more threads than RLIMIT_NPROC allows, in a child process run as an
+    unprivileged user: -1 (every started thread joined, none of the unset
+    handles), not a crash and not a 0 over a partly written output."""
+    import subprocess
+    import sys
+    from conftest import REPO
+    code = r'''
+import ctypes, os, resource, sys
+lib = ctypes.CDLL(sys.argv[1])
+vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+lib.or_synth_digests.argtypes = [u64, u64, ctypes.c_uint32, u64, vp, ctypes.c_int]
+lib.or_hash_chunks.argtypes = [vp, u64, u64, ctypes.c_uint32, ctypes.c_uint32, vp, ctypes.c_int]
+n, L = 64, 4096
+img = (ctypes.c_uint8 * (n * L))()
+out = (ctypes.c_uint8 * (20 * n))()
+ok_all = lib.or_synth_digests(0, n, L, 77, out, 8)       # unrestricted: 0
+if os.geteuid() == 0:
+    os.setgid(65534)
+    os.setuid(65534)
+resource.setrlimit(resource.RLIMIT_NPROC, (1, 1))
+print(ok_all, lib.or_synth_digests(0, n, L, 77, out, 8), lib.or_hash_chunks(img, n, L, L, L, out, 16))
+'''
+    r = subprocess.run([sys.executable, "-c", code, f"{REPO}/oracle/liboracle_sha1.so"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["0", "-1", "-1"], r.stdout

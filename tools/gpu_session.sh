@@ -2,6 +2,8 @@
 # tools/gpu_session.sh STEP... -- run GPU steps on the gpurun box, each under
 # its own time limit, stopping at the first crash/timeout/abort (never retry).
 # Steps: smoke | tests | bench | prof | pmc | residency | power | ... (see case below)
+# Steps that pass --ring/--lines/--nt to bench.py run the rejected hot-kernel
+# variants: bench.py then loads build_variants/experiments/libbtsha1.so.
 # Outputs land in gpurun_out/ (merged back by gpurun).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -40,6 +42,11 @@ for step in "$@"; do
       run "pytest_${step#pytest:}" 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         -p no:cacheprovider -k "${step#pytest:}" ;;
     bench) run bench 600 python3 bench.py ;;
+    driver_bench)
+      # the driver's exact N=1 command (BENCH_rNN.json), timed from outside as well
+      t0=$(date +%s%N)
+      run driver_bench 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
+      echo "driver_bench outer wall ms: $(( ($(date +%s%N) - t0) / 1000000 ))" | tee -a "$OUT/session.log" ;;
     bench2)
       # two default runs back to back on one box (within-box repeatability of the line)
       run bench_a 600 python3 bench.py && run bench_b 600 python3 bench.py ;;
@@ -201,19 +208,12 @@ for step in "$@"; do
         -- python3 "$ROOT/tools/stream_bench.py" 4 ;;
     latency) run latency 300 python3 tools/latency_bench.py ;;
     numa) run numa 600 python3 tools/numa_probe.py 4 ;;
-    numa_final)
-      for rep in 1 2; do
-        run "nf_default_$rep" 600 python3 tools/numa_probe.py 8 && \
-        run "nf_numa0_$rep" 600 env BT_SHA1_NUMA=0 python3 tools/numa_probe.py 8 || exit 1
-      done ;;
     copy_order)
+      # A/B of the direct-DMA copy order (bt_sha1_api.cpp serial_copies), both legs forced
       for rep in 1 2; do
-        run "co_overlap_$rep" 600 env BT_SHA1_NUMA=0 python3 tools/numa_probe.py 8 && \
-        run "co_serial_$rep" 600 env BT_SHA1_NUMA=0 BT_SHA1_COPY_ORDER=serial python3 tools/numa_probe.py 8 || exit 1
+        run "co_overlap_$rep" 600 env BT_SHA1_COPY_ORDER=overlap python3 tools/numa_probe.py 8 && \
+        run "co_serial_$rep" 600 env BT_SHA1_COPY_ORDER=serial python3 tools/numa_probe.py 8 || exit 1
       done ;;
-    numa_ab)
-      run numa_off 600 env BT_SHA1_NUMA=0 python3 tools/numa_probe.py 4 && run numa_on 600 python3 tools/numa_probe.py 4 \
-        && run numa_off8 600 env BT_SHA1_NUMA=0 python3 tools/numa_probe.py 8 && run numa_on8 600 python3 tools/numa_probe.py 8 ;;
     latency_ab)
       run latency_spin 300 python3 tools/latency_bench.py
       run latency_streamsync 300 env BT_SHA1_SYNC=stream python3 tools/latency_bench.py

@@ -5,7 +5,8 @@ from the gfx950 ISA that hipcc emits for sha1_kernels.hip.
 The hot loop of k_sha1_fixed<NBUF, L, 0, false> compresses NBUF*2L blocks per
 iteration (fully unrolled), so the per-block mix is the loop body's count
 divided by that.  Also reports the kernel's VGPR count and scratch size.
-Usage: python3 tools/isa_mix.py [NBUF L]   (default: 3 1, the library default)
+Usage: python3 tools/isa_mix.py [NBUF L]   (default: 3 1, the library default;
+other shapes are read from the experiments build)
 Prints one JSON object.  DESIGN.md §4 quotes these numbers; tests/test_isa.py
 checks them.
 """
@@ -23,9 +24,12 @@ CSRC = os.path.join(HERE, "bittorrent-with-congestion-control_amd", "csrc")
 HALF_RATE = {"v_alignbit_b32", "v_add3_u32", "v_perm_b32"}  # tools/ubench/valu_rate.hip
 
 
-def compile_asm(out):
+def compile_asm(out, experiments=False):
+    """Device ISA of sha1_kernels.hip as the product library builds it, or with
+    the rejected hot-kernel variants too (the experiments library)."""
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
                     "-I" + os.path.join(HERE, "include"), "-I" + CSRC, "--cuda-device-only", "-S",
+                    *(["-DBT_SHA1_EXPERIMENTS"] if experiments else []),
                     "-o", out, os.path.join(CSRC, "sha1_kernels.hip")],
                    check=True, capture_output=True)
 
@@ -65,7 +69,7 @@ def main():
     nbuf, lines = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (3, 1)
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "k.s")
-        compile_asm(out)
+        compile_asm(out, experiments=(nbuf, lines) != (3, 1))
         print(json.dumps(loop_mix(open(out).read(), nbuf, lines)))
 
 

@@ -54,11 +54,17 @@ const char *bt_sha1_build_info(void);
  * stripped, so comment edits keep it): ties profiles
  * (PMC traffic, rocprof summaries) to the build that produced them. */
 const char *bt_sha1_source_id(void);
-/* Hot-kernel register-ring depth in 128-byte lines (2, 3 or 4; default 3).
- * 10 selects the LDS-staged variant (coalesced loads DMA'd into LDS). */
+/* Hot-kernel register-ring depth in 128-byte lines (default 3).  The product
+ * library carries only the default hot kernel (3 slots of one line, plain
+ * loads) and accepts only 3; the measured-and-rejected variants (2 or 4
+ * slots, two-line slots, non-temporal loads, and 10 = the LDS-staged
+ * k_sha1_lds) are compiled into build_variants/experiments/libbtsha1.so
+ * (`make experiments`) alone. */
 int bt_sha1_set_ring_depth(int nbuf);
 /* Hot-kernel variant: nbuf ring slots of `lines` 128-byte lines each, nt = 1
- * for non-temporal loads.  Returns -1 for a combination not compiled in. */
+ * for non-temporal loads.  Returns -1 (message names the experiments
+ * library) for a combination this library does not carry: in the product
+ * library, anything but (3, 1, 0). */
 int bt_sha1_set_variant(int nbuf, int lines, int nt);
 /* Batches of at most max_chunks chunks take the latency kernel (a loader /
  * schedule wave and a round wave per 64 chunks, meeting in LDS), which
@@ -76,7 +82,8 @@ uint64_t bt_sha1_set_latency_batch(uint64_t max_chunks);
 uint64_t bt_sha1_set_chain_batch(uint64_t max_messages);
 /* Name of the kernel a fixed-layout batch of n_chunks chunks runs on the
  * current device ("k_sha1_chain" up to two chunks per CU, "k_sha1_lat" up to
- * the latency batch, else "k_sha1_fixed" or, with variant 10, "k_sha1_lds");
+ * the latency batch, else "k_sha1_fixed" -- or, in the experiments library
+ * with variant 10, "k_sha1_lds");
  * NULL without a device. */
 const char *bt_sha1_kernel_name(uint64_t n_chunks);
 /* Diagnostic (bench clock measurement): hashes the batch like

@@ -35,7 +35,7 @@ REF_SO = os.path.join(REPO, "oracle", "_ref", "libref_sha1.so")
 ORACLE_SO = os.path.join(REPO, "oracle", "liboracle_sha1.so")
 CHUNK = 512 * 1024
 SEED_SYNTH = 0x0B175EED
-PREFIXES = [4096, 40960 * 2, 131072, 262144, 524288, 1048576]
+PREFIXES = [4096, 40960 * 2, 131072, 262144, 40960 * 8, 524288, 1048576]
 
 
 def main():

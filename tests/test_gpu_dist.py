@@ -110,18 +110,20 @@ def test_bench_ranks_split_and_gather_on_one_gpu(world, oracle):
     _check_sample(line, world, chunks, oracle)
 
 
-@pytest.mark.parametrize("chunks", [40960, 131072])
-def test_bench_ranks_run_the_hot_kernel_with_parity_on_every_rank(oracle, chunks):
+@pytest.mark.parametrize("world,chunks", [(2, 40960), (2, 131072), (8, 40960)])
+def test_bench_ranks_run_the_hot_kernel_with_parity_on_every_rank(oracle, world, chunks):
     """Config 4's per-rank kernel through the rank path: at 40960 chunks per
     rank the batch selects k_sha1_fixed (one-wave workgroups, < 1 wave per
     SIMD), and 131072 per rank is exactly the 8-GPU bench's per-rank workload
-    (64 GiB each, 128 GiB for both ranks in the one GPU's 288 GB)."""
-    world = 2
+    (64 GiB each, 128 GiB for both ranks in the one GPU's 288 GB).  Eight
+    ranks x 40960 (160 GiB on the one GPU) is the driver's N = 8 launch with
+    every rank on the hot kernel: 327,680 digests, all compared with the
+    reference's checksum and with the oracle."""
     line = _run_bench(world, chunks, "--power-s", "0", timeout=300)
     assert line["roofline"]["kernel"] == "k_sha1_fixed"
     assert line["config"]["global_chunks"] == world * chunks
     assert line["parity_first_4096_vs_golden"] is True   # rank 0's first 4096 vs sha.c golden
-    assert [p["rank"] for p in line["per_gpu"]] == [0, 1]
+    assert [p["rank"] for p in line["per_gpu"]] == list(range(world))
     _check_identity(line, world, chunks)
     _check_sample(line, world, chunks, oracle)
 

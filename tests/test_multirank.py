@@ -258,3 +258,39 @@ def test_bench_cpu_baseline_leg(oracle):
     bad = bytearray(want)
     bad[0] ^= 1
     assert bench.cpu_baseline(ctypes.addressof(buf), n, bytes(bad), min_s=0.01, reps=1)["digests_match_gpu"] is False
+
+
+def _bench_module():
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+def test_bench_traffic_lookup_needs_the_same_build(tmp_path):
+    """roofline.traffic is reported only from a PMC file measured on this very
+    source id, kernel, variant and layout; a file from another build (e.g. a
+    diagnostic build's suffixed id) yields null and says why."""
+    import json
+    bench = _bench_module()
+    want = {"chunks": 131072, "pitch": 524288, "source_id": "abc", "kernel": "k_sha1_fixed", "variant": "310"}
+    p = tmp_path / "traffic_r09.json"
+    p.write_text(json.dumps({**want, "hbm_bytes_per_launch": 6.9e10}))
+    assert bench.find_traffic(want, str(p)) == (6.9e10, f"{os.path.relpath(str(p), REPO)} (rocprofv3 --pmc, same source id)")
+    t, note = bench.find_traffic({**want, "source_id": "abc-dbgbar"}, str(p))
+    assert t is None and "another build" in note and "abc-dbgbar" in note
+    # default: the committed traffic files; the newest one matching the product build wins
+    files = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.startswith("traffic_r"))
+    newest = json.load(open(os.path.join(REPO, "profiles", files[-1])))
+    mine = {k: newest[k] for k in want}
+    t, note = bench.find_traffic(mine)
+    assert t == newest["hbm_bytes_per_launch"] and files[-1] in note
+
+
+def test_bench_process_age_is_wall_time_since_start():
+    import time
+    bench = _bench_module()
+    a = bench.process_age_s()
+    time.sleep(0.3)
+    b = bench.process_age_s()
+    assert 0 <= a < 600 and 0.2 <= b - a <= 2.0

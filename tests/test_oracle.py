@@ -106,7 +106,7 @@ def test_batch_checksums_are_the_reference_digests(oracle):
     smaller rows; the config-4 row (1,048,576 chunks) is what bench.py's
     parity_all_vs_golden compares an 8-GPU run with."""
     table = dict(read_pairs("synth_checksums.txt"))
-    assert {"4096", "81920", "131072", "262144", "524288", "1048576"} <= set(table)
+    assert {"4096", "81920", "131072", "262144", "327680", "524288", "1048576"} <= set(table)
     rows = read_pairs("synth4096.txt")
     assert hashlib.sha1(b"".join(bytes.fromhex(h) for _, h in rows)).hexdigest() == table["4096"]
     assert hashlib.sha1(oracle.synth_digests(0, 81920)).hexdigest() == table["81920"]

@@ -316,15 +316,20 @@ int launch_image(const uint8_t *d_img, uint64_t bytes, uint64_t chunk_len, uint8
 // wave per SIMD) still outruns PCIe; capped by the input size when known.  An
 // input of 64 MiB - 2 GiB is cut in two batches so both lanes work (the second
 // lane's pinning overlaps the first batch, see run_pipeline).
-// Direct-DMA input (pinned / registered) uses bigger batches: there is no
-// staging copy to overlap, only the per-transfer cost of DMA from registered
-// memory to amortise (8 GiB registered image, same box: 40.2 / 45.9 / 48.9
-// GiB/s with 1 / 2 / 4 GiB batches; one 8 GiB copy alone: 53.6).
-// BT_SHA1_DMA_BATCH_MB overrides the 4096 MiB default.
+// Direct-DMA input (pinned / registered) uses the same 1 GiB batches, DMA'd
+// straight from the caller's memory into the kept lanes.  Round 2 chose 4 GiB
+// batches under overlapping copies (40.2 / 45.9 / 48.9 GiB/s with 1 / 2 / 4
+// GiB); with round 3's serial copy order bigger batches gain nothing, and
+// because they exceed the kept lanes they were allocated and freed on every
+// call -- and a re-allocated 4 GiB batch ran the copies at 41.1-41.4 GiB/s call
+// after call on three of three boxes (tools/dma_repeat.py;
+// profiles/r04/dma_batch.md) where 1 GiB kept lanes hold 48.9-50.7 (8 GiB
+// image) and 52.4-52.5 (32 GiB) against a ~53.6 raw copy.  BT_SHA1_DMA_BATCH_MB overrides the 1024 MiB
+// default; batches above 1 GiB are freed after the call.
 uint64_t dma_batch_target() {
   static const uint64_t v = [] {
     const char *e = getenv("BT_SHA1_DMA_BATCH_MB");
-    const long mb = e ? atol(e) : 4096;
+    const long mb = e ? atol(e) : 1024;
     return (uint64_t)(mb < 64 ? 64 : (mb > 16384 ? 16384 : mb)) << 20;
   }();
   return v;
@@ -568,9 +573,9 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   if (join_pre()) return -1;  // input shorter than the size hint
   // Older lane first so digests arrive in order.
   if (drain(c->lane[k & 1]) || drain(c->lane[(k + 1) & 1])) return -1;
-  // Direct-DMA batches (up to BT_SHA1_DMA_BATCH_MB, 4 GiB by default) are not
-  // kept past the call: the lanes keep at most a staged batch (1 GiB) of HBM
-  // each, so a process that shares the GPU does not lose 8 GiB for good.
+  // Direct-DMA batches bigger than a staged batch (BT_SHA1_DMA_BATCH_MB >
+  // 1024) are not kept past the call: the lanes keep at most 1 GiB of HBM
+  // each, so a process that shares the GPU does not lose more for good.
   if (!staged)
     for (auto &l : c->lane)
       if (l.d_in.cap > batch_bytes_for(chunk_len, UINT64_MAX, true)) l.d_in.release();

@@ -136,12 +136,11 @@ int bt_sha1_host_unregister(void *h_ptr);
  * Memory kept between calls: each device's context keeps its two staging
  * lanes, grown on demand and reused by later calls -- up to 2 x 1 GiB of
  * page-locked host memory (pageable input) and 2 x 1 GiB of HBM.  Pinned or
- * registered input is DMA'd in bigger batches (BT_SHA1_DMA_BATCH_MB, 4 GiB
- * by default); those HBM batches are freed before the call returns.  Freeing
- * them (hipFree) synchronises the whole device: such a call returns only
- * after work other streams of this process queued on the GPU has finished,
- * and callers that share the GPU with latency-sensitive streams should hash
- * pinned input in pieces of <= 2 GiB (kept lanes, no free) or use staging. */
+ * registered input is DMA'd straight from the caller's memory into the same
+ * HBM lanes (1 GiB batches).  With BT_SHA1_DMA_BATCH_MB above 1024 the
+ * direct-DMA batches are bigger and freed before the call returns; freeing
+ * them (hipFree) synchronises the whole device, so such a call returns only
+ * after work other streams of this process queued on the GPU has finished. */
 int64_t bt_sha1_chunks_host(const void *h_in, uint64_t total_len, uint64_t chunk_len,
                             uint8_t *h_digests);
 /* The same split over the first `ndev` GPUs (<=0: all), one host thread per

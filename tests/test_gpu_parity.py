@@ -520,41 +520,6 @@ def test_registered_host_image_direct_dma(bt, oracle):
         bt.host_unregister(addr)
 
 
-def test_host_calls_give_their_hbm_back(bt, torch, oracle):
-    """HBM a host call holds beyond the device context's kept staging lanes
-    (2 x <= 1 GiB, include/bt_sha1.h) is freed before it returns: the
-    direct-DMA batches of a registered image (2 GiB per lane here) and the
-    worker contexts of repeated device ids (devs=[0,0,0]), registered and
-    pageable.  hipMemGetInfo after each call against the level after a first
-    pageable call that sized the kept lanes."""
-    import numpy as np
-    n = 8192  # 4 GiB: two direct-DMA batches of 2 GiB, two staged lanes of 1 GiB
-    img = np.empty(n * CHUNK, dtype=np.uint8)
-    words = img.view(np.uint64)
-    words[:] = np.arange(words.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
-    addr = img.ctypes.data
-    want = bt.chunks_host_addr(addr, img.nbytes)                 # pageable: sizes the kept lanes
-    for i in (0, 4097, n - 1):
-        assert want[20 * i:20 * i + 20] == oracle.sha1(img[i * CHUNK:(i + 1) * CHUNK].tobytes()), i
-    torch.cuda.synchronize()
-    kept = torch.cuda.mem_get_info()[0]
-    slack = 64 << 20
-
-    def free_now():
-        torch.cuda.synchronize()
-        return torch.cuda.mem_get_info()[0]
-    assert bt.chunks_host_addr(addr, img.nbytes, devs=[0, 0, 0]) == want    # pageable, 3 workers
-    assert free_now() >= kept - slack
-    bt.host_register(addr, img.nbytes)
-    try:
-        assert bt.chunks_host_addr(addr, img.nbytes) == want                 # direct DMA, 2 GiB batches
-        assert free_now() >= kept - slack
-        assert bt.chunks_host_addr(addr, img.nbytes, devs=[0, 0, 0]) == want  # registered, 3 workers
-        assert free_now() >= kept - slack
-    finally:
-        bt.host_unregister(addr)
-
-
 def test_verify_stream_zero_copy_mode(tmp_path):
     exe = os.path.join(PKG, "bin", "verify-stream")
     p = tmp_path / "C.tar"

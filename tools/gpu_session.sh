@@ -192,6 +192,15 @@ for step in "$@"; do
       for mb in 1024 2048 4096 1024 2048 4096; do
         run "dma_batch_$mb" 300 env BT_SHA1_DMA_BATCH_MB=$mb python3 tools/stream_bench.py 8
       done ;;
+    dma_repeat)
+      # direct-DMA batch size vs run-to-run rate of the registered path (round 4):
+      # call after call in one process, and per NUMA node of the image
+      for mb in 4096 1024 2048; do
+        run "dr8_$mb" 300 env BT_SHA1_DMA_BATCH_MB=$mb python3 tools/dma_repeat.py 8 5 && \
+        run "numa8_$mb" 300 env BT_SHA1_DMA_BATCH_MB=$mb python3 tools/numa_probe.py 8 || exit 1
+      done
+      run dr32_4096 300 env BT_SHA1_DMA_BATCH_MB=4096 python3 tools/dma_repeat.py 32 4 && \
+      run dr32_1024 300 env BT_SHA1_DMA_BATCH_MB=1024 python3 tools/dma_repeat.py 32 4 ;;
     filebench) run filebench 600 env BT_SHA1_TRACE=1 python3 tools/file_bench.py /dev/shm 1 1024 8192 32768 ;;
     filethreads)
       for t in 8 12 16 8 12 16; do

@@ -76,3 +76,54 @@ def test_checked_hex(bt):
     for bad in ["0g", "zz", "1", " 1"]:
         with pytest.raises(ValueError):
             bt.hex2binary_checked(bad)
+
+
+CHUNKS_REF = os.path.join(os.path.dirname(GOLDEN), "..", "oracle", "_ref", "chunks-ref")
+
+
+def _ref_table(mode, path):
+    """The reference's own parser (util.c, compiled by oracle/Makefile) on a file."""
+    import subprocess
+    out = subprocess.run([CHUNKS_REF, mode, str(path)], capture_output=True, text=True, check=True).stdout.split("\n")
+    n = int(out[0])
+    return [(int(i), bytes.fromhex(h)) for i, h in (l.split() for l in out[1:1 + n])]
+
+
+def _entries_and_text(data):
+    """Well-formed .chunks bodies the reference parses without undefined
+    behaviour: "<id><ws><40 hex>" lines, any hex case, spaces or tabs, LF or
+    CRLF, the last line with or without its newline."""
+    from hypothesis import strategies as st
+    line = st.tuples(st.integers(-2**31, 2**31 - 1), st.binary(min_size=20, max_size=20),
+                     st.sampled_from(["lower", "upper", "mixed"]), st.sampled_from([" ", "  ", "\t", " \t "]),
+                     st.sampled_from(["\n", "\r\n", " \n"]))
+    lines = data.draw(st.lists(line, min_size=0, max_size=60))
+    text, entries = "", []
+    for k, (i, h, case, ws, eol) in enumerate(lines):
+        hx = h.hex()
+        hx = hx.upper() if case == "upper" else (
+            "".join(c.upper() if j % 2 else c for j, c in enumerate(hx)) if case == "mixed" else hx)
+        text += f"{i}{ws}{hx}" + ("" if k == len(lines) - 1 and data.draw(st.booleans()) else eol)
+        entries.append((i, h))
+    return entries, text
+
+
+@pytest.mark.skipif(not os.path.exists(CHUNKS_REF), reason="oracle/_ref/chunks-ref not built (no reference sources)")
+def test_parsers_agree_with_the_reference_parsers(bt, tmp_path_factory):
+    """Differential, property-based: libbtsha1's has/get and master parsers
+    against the reference's parse_has_get_chunk_file / parse_total_chunk_file
+    (util.c:64-164, compiled unmodified) on random well-formed files."""
+    from hypothesis import given, settings, strategies as st
+
+    @settings(max_examples=80, deadline=None)
+    @given(st.data())
+    def check(data):
+        entries, body = _entries_and_text(data)
+        d = tmp_path_factory.mktemp("fz")
+        lst, master = d / "x.chunks", d / "m.chunks"
+        lst.write_text(body)
+        master.write_text("File: some.tar\nChunks:\n" + body)
+        assert bt.parse_chunk_list(lst) == _ref_table("list", lst) == entries
+        name, got = bt.parse_master(master)
+        assert name == "some.tar" and got == _ref_table("master", master) == entries
+    check()

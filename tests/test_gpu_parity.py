@@ -622,6 +622,39 @@ def test_digest_lookup_matches_first_match_scan(bt, torch, n_table, n_query):
     assert out.cpu().tolist() == [first.get(q, -1) for q in queries]
 
 
+@pytest.mark.parametrize("n_table", [1, 1000, 20000])
+def test_digest_lookup_matches_the_reference_get_chunk_id(bt, torch, tmp_path, n_table):
+    """Differential against the reference itself: util.c's get_chunk_id
+    (util.c:28-39, compiled unmodified into oracle/_ref/chunks-ref) over a
+    master file it parsed (util.c:113-164) with duplicate digests and
+    shuffled ids, against bt_sha1_lookup_dev on the same table -- the id of
+    the FIRST matching entry, or -1 for a miss."""
+    import hashlib
+    exe = os.path.join(REPO, "oracle", "_ref", "chunks-ref")
+    assert os.path.exists(exe), "oracle/_ref/chunks-ref missing: build it with `make -C oracle` where the reference exists"
+    rng = random.Random(1000 + n_table)
+    distinct = [hashlib.sha1(b"t" + str(i).encode()).digest() for i in range(max(1, n_table * 2 // 3))]
+    table = [distinct[rng.randrange(len(distinct))] for _ in range(n_table)]
+    ids = list(range(n_table))
+    rng.shuffle(ids)
+    master = tmp_path / "m.chunks"
+    master.write_text("File: x.tar\nChunks:\n" + "".join(f"{i} {h.hex()}\n" for i, h in zip(ids, table)))
+    queries = [table[rng.randrange(n_table)] if rng.random() < 0.7 else hashlib.sha1(b"q" + str(k).encode()).digest()
+               for k in range(3000)]
+    qf = tmp_path / "q.txt"
+    qf.write_text("".join(q.hex() + "\n" for q in queries))
+    ref = [int(x) for x in subprocess.run([exe, "lookup", str(master), str(qf)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    name, entries = bt.parse_master(str(master))
+    dt = _dev_bytes(torch, b"".join(h for _, h in entries))
+    dq = _dev_bytes(torch, b"".join(queries))
+    out = torch.full((len(queries),), 7, dtype=torch.int64, device="cuda")
+    bt.lookup_dev(dt.data_ptr(), len(entries), dq.data_ptr(), len(queries), out.data_ptr())
+    torch.cuda.synchronize()
+    got = [entries[i][0] if i >= 0 else -1 for i in out.cpu().tolist()]
+    assert len(ref) == len(queries) and got == ref
+
+
 def test_parse_then_lookup_then_verify_c_tar(bt, torch):
     """The peer's flow on the reference fixtures: master file -> GPU lookup of
     the has-file hashes -> verify the C.tar chunks against the master."""

@@ -394,6 +394,28 @@ def test_reference_make_chunks_linked_to_dropin(tmp_path):
     assert out == open(os.path.join(GOLDEN, "C.tar.make-chunks.out")).read()
 
 
+@pytest.mark.parametrize("size", [0, 1, 55, 56, 63, 64, 65, CHUNK - 1, CHUNK, CHUNK + 1, 3 * CHUNK + 12345,
+                                  33 * CHUNK - 7, 64 * CHUNK + 64 * 1024 + 56, 200 * CHUNK + 1])
+def test_make_chunks_three_ways_on_random_sizes(tmp_path, oracle, size):
+    """make-chunks stdout, byte for byte, three ways on the same file: the
+    reference binary itself (make_chunks.c + chunk.c + sha.c on the CPU,
+    oracle/_ref/make-chunks), the reference's make_chunks.c linked to
+    libbtsha1.so (oracle/_ref/make-chunks-dropin) and our CLI -- sizes around
+    the MD padding boundaries (55/56/63/64 bytes into a block) and the chunk
+    boundary, with short last chunks riding in the same launch (chunk.c:20)."""
+    ref = os.path.join(REPO, "oracle", "_ref", "make-chunks")
+    dropin = os.path.join(REPO, "oracle", "_ref", "make-chunks-dropin")
+    ours = os.path.join(PKG, "bin", "make-chunks")
+    for exe in (ref, dropin):
+        assert os.path.exists(exe), f"{exe} missing: built by oracle/Makefile / make dropin where the reference exists"
+    p = tmp_path / "f.bin"
+    p.write_bytes(bytes(oracle.fill_synthetic(size, size, 0x3A4E)))
+    env = dict(os.environ, LD_LIBRARY_PATH=PKG + ":" + os.environ.get("LD_LIBRARY_PATH", ""))
+    outs = [subprocess.run([exe, str(p)], capture_output=True, check=True, env=env).stdout for exe in (ref, dropin, ours)]
+    assert outs[0] == outs[1] == outs[2], size
+    assert outs[0].count(b"\n") == (size + CHUNK - 1) // CHUNK
+
+
 def test_reference_save_chunk_linked_to_dropin(tmp_path):
     """Caller #2 at the boundary: the reference peer's own util.c (save_data_packet
     util.c:250-277 + save_chunk util.c:304-337) and file.c, compiled unmodified
@@ -919,6 +941,43 @@ def test_streaming_update_pieces_and_context(bt, oracle):
             assert list(s.ctx.hash) == oracle.compress_blocks(
                 [0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476, 0xc3d2e1f0], msg[:done]), k
     assert s.final() == o.final() == oracle.sha1(msg)
+
+
+def test_streaming_context_equals_the_reference_context(bt, oracle):
+    """The drop-in's SHA1Context against the REFERENCE's own (sha.c's
+    SHA1Init / SHA1Update / SHA1Final, compiled into oracle/_ref/libref_sha1.so,
+    same 96-byte layout, sha.h:39-50): after every SHA1Update of random length
+    (0..5000 bytes, so calls end at every offset within a block and some carry
+    no whole block) the two contexts agree on totalLength, hash[5],
+    bufferLength and the buffered bytes; the digests agree at the end."""
+    ref_path = os.path.join(REPO, "oracle", "_ref", "libref_sha1.so")
+    assert os.path.exists(ref_path), "oracle/_ref/libref_sha1.so missing: built by oracle/Makefile"
+    ref = ctypes.CDLL(ref_path)
+    ctx_t = bt.SHA1Context
+    ref.SHA1Init.argtypes = [ctypes.POINTER(ctx_t)]
+    ref.SHA1Update.argtypes = [ctypes.POINTER(ctx_t), ctypes.c_void_p, ctypes.c_uint32]
+    ref.SHA1Final.argtypes = [ctypes.POINTER(ctx_t), ctypes.c_void_p]
+    rng = random.Random(4242)
+    for trial in range(3):
+        msg = bytes(oracle.fill_synthetic(150000 + trial * 7919, trial, 0x5EED))
+        rc = ctx_t()
+        ref.SHA1Init(ctypes.byref(rc))
+        s = bt.Sha1()
+        i = calls = 0
+        while i < len(msg):
+            j = min(len(msg), i + rng.choice([0, 1, 55, 56, 63, 64, 65, rng.randrange(5000)]))
+            piece = msg[i:j]
+            buf = (ctypes.c_uint8 * max(1, len(piece))).from_buffer_copy(piece or b"\0")
+            ref.SHA1Update(ctypes.byref(rc), buf, len(piece))
+            s.update(piece)
+            i, calls = j, calls + 1
+            n = rc.bufferLength
+            assert (s.ctx.totalLength, list(s.ctx.hash), s.ctx.bufferLength) == \
+                (rc.totalLength, list(rc.hash), n), (trial, calls, i)
+            assert bytes(s.ctx.buffer[:n]) == bytes(rc.buffer[:n]), (trial, calls, i)
+        out = (ctypes.c_uint8 * 20)()
+        ref.SHA1Final(ctypes.byref(rc), out)
+        assert s.final() == bytes(out) == oracle.sha1(msg), trial
 
 
 def test_dropin_calls_from_many_threads(bt, oracle):

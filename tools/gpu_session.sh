@@ -110,6 +110,15 @@ for step in "$@"; do
     occupancy)
       run occ_262144 300 python3 bench.py --ring 2 --chunks 262144 --steps 5 --no-cpu-baseline
       run occ_393216 300 python3 bench.py --ring 2 --chunks 393216 --steps 5 --no-cpu-baseline ;;
+    occupancy2)
+      # round 4: parallelism beyond the workload's 2 waves/SIMD, same box, alternating:
+      # one launch of 131072 chunks, one of 262144, two concurrent processes of 131072
+      B="python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-path"
+      for rep in 1 2; do
+        run "occ_n1_$rep" 200 $B && run "occ_n1_262k_$rep" 200 $B --chunks 262144 && \
+        run "occ_n2_$rep" 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+          --master-port 2955$rep bench.py --gpus 2 --steps 20 --warmup 5 || exit 1
+      done ;;
     counters) run counters 120 rocprofv3 -L ;;
     residency) run residency 300 "$ROOT/tools/ubench/residency" ;;
     power_residency)

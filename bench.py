@@ -37,6 +37,8 @@ import importlib.util
 import json
 import math
 import os
+import signal
+import socket
 import subprocess
 import sys
 import tempfile
@@ -86,18 +88,111 @@ def _load(name, path):
     return mod
 
 
-def ensure_built():
+EXPERIMENTS_LIB = os.path.join(HERE, "build_variants", "experiments", "libbtsha1.so")
+
+
+def ensure_built(experiments=False):
     """A clean checkout has no built artefacts (git-ignored): build the library,
-    its host tools and the test-only oracle once (N ranks start together)."""
+    its host tools and the test-only oracle once (N ranks start together) --
+    and, for a non-default --ring/--lines/--nt variant, the experiments library
+    that alone carries the rejected hot-kernel variants."""
     need = [os.path.join(PKG, "libbtsha1.so"), os.path.join(PKG, "bin", "verify-stream"),
             os.path.join(HERE, "oracle", "liboracle_sha1.so"), os.path.join(HERE, "oracle", "liboracle_sha1_O0.so")]
+    targets = ["lib", "tools", "oracle"]
+    if experiments:
+        need.append(EXPERIMENTS_LIB)
+        targets.append("experiments")
     if all(os.path.exists(p) for p in need):
         return
     import fcntl
     with open(os.path.join(HERE, ".build.lock"), "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
         if not all(os.path.exists(p) for p in need):
-            subprocess.run(["make", "-C", HERE, "-j8", "lib", "tools", "oracle"], check=True)
+            subprocess.run(["make", "-C", HERE, "-j8", *targets], check=True)
+
+
+# ---------------------------------------------------------------------------
+# --gpus N is authoritative (the driver's `python bench.py --gpus N` and its
+# torchrun launch both end up as N ranks, or the run fails before any GPU call)
+# ---------------------------------------------------------------------------
+def rank_plan(gpus, environ):
+    """("single" | "spawn" | "ranks", error message or None) for `--gpus
+    gpus` under `environ` -- decided before torch is imported:
+      * WORLD_SIZE unset, gpus == 1: this process is the one rank;
+      * WORLD_SIZE unset, gpus > 1: start the N ranks as a torch.distributed.run
+        child (spawn_ranks) and relay rank 0's line;
+      * WORLD_SIZE set: a launcher started us as one of its ranks, and its
+        world size must be exactly --gpus (a mismatch is a launch error: the
+        line would claim a GPU count it did not run on)."""
+    if gpus < 1:
+        return None, f"--gpus {gpus}: need at least one GPU"
+    ws = environ.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        return ("single" if gpus == 1 else "spawn"), None
+    try:
+        world = int(ws)
+    except ValueError:
+        return None, f"WORLD_SIZE={ws!r} is not an integer"
+    if world != gpus:
+        return None, (f"launched as one of WORLD_SIZE={world} ranks but --gpus {gpus}: the launcher's world size and "
+                      f"--gpus must agree (run `python bench.py --gpus {gpus}` alone, or launch {gpus} ranks)")
+    return "ranks", None
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(n, argv, port):
+    """The driver's own N > 1 launch line (one process per GPU, 127.0.0.1
+    rendezvous), running this file with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def relay(cmd, env=None):
+    """Run `cmd` as a child process (never exec: nothing here has touched the
+    GPU, but the ranks will) and relay its result line: the child's JSON
+    line(s) are held back and exactly one is printed on our stdout; every
+    other stdout line goes to stderr as it arrives, stderr passes straight
+    through (progress stays visible).  SIGTERM is forwarded to the child, and
+    the child gets SIGTERM if this process dies (PR_SET_PDEATHSIG), so the
+    ranks never outlive their parent.  Returns the child's exit status, or 1
+    when it exited 0 without exactly one JSON line."""
+    def die_with_parent():
+        ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGTERM))  # PR_SET_PDEATHSIG
+
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1, preexec_fn=die_with_parent)
+    prev = signal.signal(signal.SIGTERM, lambda sig, _frame: p.send_signal(sig))
+    lines = []
+    try:
+        for text in p.stdout:
+            if text.startswith("{"):
+                lines.append(text.rstrip("\n"))
+            else:
+                sys.stderr.write(text)
+                sys.stderr.flush()
+        rc = p.wait()
+    finally:
+        signal.signal(signal.SIGTERM, prev)
+    if len(lines) == 1:
+        print(lines[0], flush=True)
+    elif rc == 0:
+        print(f"bench.py: the rank launch printed {len(lines)} result lines, expected exactly 1", file=sys.stderr,
+              flush=True)
+        return 1
+    return rc
+
+
+def spawn_ranks(n, argv):
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool
+    cmd = rank_launch_cmd(n, argv, free_port())
+    print(f"bench.py: --gpus {n} without a launcher: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr,
+          flush=True)
+    return relay(cmd, env)
 
 
 # ---------------------------------------------------------------------------
@@ -145,37 +240,63 @@ class DeviceHasher:
     def digests(self):
         return self.dig.cpu().numpy().tobytes()
 
-    def verify_rate(self, reps=5):
+    def verify_rate(self, pairs=6):
         """Device-resident verify (util.c:311-313's hash + memcmp, batched):
         bt_sha1_verify_dev over the same chunks against expected digests in
-        HBM, every 997th deliberately wrong; HIP-event time per pass on the
-        hasher's stream (after one untimed pass: the first launch of the
-        verify instantiation pays a one-time cost, ~3 ms in rocprof traces)
-        and whether exactly the wrong ones were flagged."""
+        HBM, every 997th deliberately wrong, measured PAIRED with the plain
+        hash it extends: `pairs` pairs of one chunks_dev and one verify_dev
+        launch, interleaved on the hasher's stream in one window in ABBA order
+        (hash-verify, verify-hash, ...) so clock / power drift falls on both
+        kernels alike, each launch timed with its own HIP events.  One untimed
+        launch of each first (the first launch of the verify instantiation
+        pays a one-time cost, ~3 ms in rocprof traces).  Reports both means,
+        the overhead of the fused compare and its spread over the pairs, and
+        whether exactly the wrong chunks were flagged."""
+        import statistics
         torch = self.torch
+        ev = torch.cuda.Event
         with torch.cuda.stream(self.stream):
             exp = self.dig.clone()
             bad = torch.arange(0, self.C, 997, device="cuda")
             exp.view(-1, 20)[bad, 0] ^= 1
             ok = torch.full((self.C,), 7, dtype=torch.uint8, device="cuda")
-            self.bt.verify_dev(self.buf.data_ptr(), self.C, CHUNK, self.pitch, exp.data_ptr(), ok.data_ptr(),
-                               None, self.sp)
+
+            def launch(kind):
+                if kind == "verify":
+                    self.bt.verify_dev(self.buf.data_ptr(), self.C, CHUNK, self.pitch, exp.data_ptr(),
+                                       ok.data_ptr(), None, self.sp)
+                else:
+                    self.bt.chunks_dev(self.buf.data_ptr(), self.C, CHUNK, self.pitch, self.dig.data_ptr(), self.sp)
+            launch("verify")
+            launch("hash")
             ok.fill_(7)  # the timed passes must set every flag themselves
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(self.stream)
-            for _ in range(reps):
-                self.bt.verify_dev(self.buf.data_ptr(), self.C, CHUNK, self.pitch, exp.data_ptr(), ok.data_ptr(),
-                                   None, self.sp)
-            b.record(self.stream)
+            timed = []
+            for p in range(pairs):
+                for kind in (("hash", "verify") if p % 2 == 0 else ("verify", "hash")):
+                    a, b = ev(enable_timing=True), ev(enable_timing=True)
+                    a.record(self.stream)
+                    launch(kind)
+                    b.record(self.stream)
+                    timed.append((p, kind, a, b))
         torch.cuda.synchronize()
-        ms = a.elapsed_time(b) / reps
+        ms = {(p, k): a.elapsed_time(b) for p, k, a, b in timed}
+        hash_ms = [ms[(p, "hash")] for p in range(pairs)]
+        ver_ms = [ms[(p, "verify")] for p in range(pairs)]
+        per_pair = [100.0 * (v / h - 1.0) for h, v in zip(hash_ms, ver_ms)]
+        h_mean, v_mean = statistics.mean(hash_ms), statistics.mean(ver_ms)
         want = torch.ones(self.C, dtype=torch.uint8, device="cuda")
         want[bad] = 0
-        return {"GiB_per_s": round(self.C * CHUNK / (ms * 1e-3) / 2**30, 3), "kernel_ms": round(ms, 4),
+        return {"GiB_per_s": round(self.C * CHUNK / (v_mean * 1e-3) / 2**30, 3), "kernel_ms": round(v_mean, 4),
+                "hash_ms": round(h_mean, 4), "verify_ms": round(v_mean, 4),
+                "overhead_pct": round(100.0 * (v_mean / h_mean - 1.0), 3),
+                "overhead_pct_pairs": {"min": round(min(per_pair), 3), "median": round(statistics.median(per_pair), 3),
+                                       "max": round(max(per_pair), 3)},
+                "pairs": pairs,
                 "flags_correct": bool(torch.equal(ok, want)), "mismatches_planted": int(bad.numel()),
                 "kernel": self.bt.kernel_name(self.C),
                 "path": "bt_sha1_verify_dev: the hot kernel with its fused compare epilogue (util.c:311-313) "
-                        "against expected digests in HBM, one launch per pass, one untimed pass first"}
+                        "against expected digests in HBM, paired with bt_sha1_chunks_dev in one window (ABBA "
+                        "order, per-launch HIP events on the hasher's stream), one untimed launch of each first"}
 
     def clock_mhz(self, launches=3):
         """Median in-kernel shader clock over the waves of the last of
@@ -216,14 +337,16 @@ def _smi_handle(torch, dev):
 
 
 def device_identity(torch, dev):
-    """Which physical GPU this rank drives: its PCI address (domain:bus:device.0,
-    as HIP reports it) and the UUID amdsmi holds for that address (the
-    `uuid` HIP exposes through torch as a fallback), the HIP device index, and
-    how many devices the rank can see -- so an N > 1 line proves it ran on N
-    distinct GPUs (shard.check_distinct_devices)."""
+    """Which physical GPU this rank drives: its host, its PCI address
+    (domain:bus:device.0, as HIP reports it) and the UUID amdsmi holds for
+    that address (the `uuid` HIP exposes through torch as a fallback), the HIP
+    device index, and how many devices the rank can see -- so an N > 1 line
+    proves it ran on N distinct GPUs (shard.check_distinct_devices; the host
+    keeps two nodes' equal PCI addresses apart)."""
     p = torch.cuda.get_device_properties(dev)
     ident = {"pci_bdf": f"{int(p.pci_domain_id):04x}:{int(p.pci_bus_id):02x}:{int(p.pci_device_id):02x}.0",
-             "uuid": None, "hip_device": dev, "device_count": torch.cuda.device_count(), "name": p.name}
+             "uuid": None, "hip_device": dev, "device_count": torch.cuda.device_count(), "name": p.name,
+             "host": socket.gethostname()}
     smi = None
     try:
         smi, h = _smi_handle(torch, dev)
@@ -554,7 +677,18 @@ def main():
     ap.add_argument("--digest-sample", type=int, default=3,
                     help="digests of this many chunks of EVERY rank (first, last, evenly between) in the line, "
                          "for parity checks beyond the golden range (0 = off)")
+    ap.add_argument("--rehearse-shared-gpu", action="store_true",
+                    help="allow N > 1 ranks on fewer than N distinct GPUs (a rehearsal of the rank path on one "
+                         "GPU, recorded in the line); without it such a launch exits before the timed region")
     args = ap.parse_args()
+
+    # Before torch is imported or any GPU call: --gpus decides the rank count.
+    plan, err = rank_plan(args.gpus, os.environ)
+    if err:
+        print(f"bench.py: {err}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
@@ -580,13 +714,14 @@ def main():
             group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group(args.backend)
-    if rank == 0:
-        ensure_built()
-    shard.barrier(world, group)
     variant = (args.ring, args.lines, args.nt) if args.ring else DEFAULT_VARIANT
-    if variant != DEFAULT_VARIANT and "BT_SHA1_LIB" not in os.environ:
+    experiments = variant != DEFAULT_VARIANT and "BT_SHA1_LIB" not in os.environ
+    if rank == 0:
+        ensure_built(experiments)
+    shard.barrier(world, group)
+    if experiments:
         # the rejected hot-kernel variants exist only in the experiments build
-        os.environ["BT_SHA1_LIB"] = os.path.join(HERE, "build_variants", "experiments", "libbtsha1.so")
+        os.environ["BT_SHA1_LIB"] = EXPERIMENTS_LIB
     bt = _load("btsha1", os.path.join(PKG, "btsha1.py"))
     if args.ring:
         bt.set_variant(*variant)
@@ -598,7 +733,7 @@ def main():
     # N > 1 line must show N distinct devices (PCI address + UUID per rank).
     ident = dict(rank=rank, **device_identity(torch, dev), kernel=kernel, chunk_range=[first_chunk, last_chunk])
     idents = shard.gather_objects(ident, world, group)
-    clash = shard.check_distinct_devices(idents, world)
+    clash = shard.check_distinct_devices(idents, world, allow_shared=args.rehearse_shared_gpu)
     if clash:
         print(f"bench.py rank {rank}: {clash}", file=sys.stderr, flush=True)
         if world > 1:
@@ -610,16 +745,33 @@ def main():
     res = shard.run_rank(hasher, args.steps, args.warmup, world, rank, group)
     phase("warmup_and_timed_s")
 
-    clock = None
-    if world == 1 and not args.no_clock and kernel == "k_sha1_fixed":
+    # Every rank stamps its own GPU's in-kernel clock (all ranks together,
+    # after the timed region), so a slow rank of an N-GPU line is attributable
+    # to its clock or to its kernel without a second run.
+    clock, rank_mhz = None, None
+    if not args.no_clock and kernel == "k_sha1_fixed":
+        mine, err = [-1.0, 0.0], None
         try:
             mhz, same = hasher.clock_mhz()
-            clock = {"in_kernel_mhz": round(mhz, 1), "probe_digests_identical": same,
+            mine = [mhz, 1.0 if same else 0.0]
+        except Exception as e:  # noqa: BLE001 -- the clock evidence must never cost the bench line
+            err = f"{type(e).__name__}: {e}"
+        allc = shard.gather_floats(mine, world, group)
+        rank_mhz = [round(m, 1) if m > 0 else None for m, _ in allc]
+        ok = [m for m in rank_mhz if m is not None]
+        if ok:
+            slow = min(range(world), key=lambda r: rank_mhz[r] if rank_mhz[r] is not None else math.inf)
+            clock = {"in_kernel_mhz": min(ok), "probe_digests_identical": all(s > 0 for _, s in allc),
                      "method": "stamped build of the hot kernel (bt_sha1_clock_probe): median over waves of "
                                "delta s_memtime / delta s_memrealtime x wall-clock rate, 3 launches after the "
-                               "timed region"}
-        except Exception as e:  # noqa: BLE001 -- the clock evidence must never cost the bench line
-            clock = {"error": f"{type(e).__name__}: {e}"}
+                               "timed region, on every rank"}
+            if world > 1:
+                clock.update(slowest_rank=slow, per_rank_mhz=rank_mhz,
+                             note="in_kernel_mhz = the slowest rank's clock (it prices the VALU roofline)")
+            if len(ok) < world:
+                clock["missing_ranks"] = [r for r in range(world) if rank_mhz[r] is None]
+        else:
+            clock = {"error": err or "no rank reported a clock"}
         phase("clock_s")
 
     # Every rank measures its own GPU's power (all ranks run the window together).
@@ -769,8 +921,10 @@ def main():
             # per rank: its rate and kernel time, and which GPU it was (PCI address,
             # UUID, devices visible), which kernel it ran and on which global chunks
             "per_gpu": [{**idents[r], "GiB_per_s": round(C * CHUNK * args.steps / w / 2**30, 3),
-                         "kernel_ms": round(k, 4)} for r, (w, k) in enumerate(res["per_rank"])],
-            "distinct_gpus": len({i["pci_bdf"] for i in idents}),
+                         "kernel_ms": round(k, 4), "in_kernel_mhz": rank_mhz[r] if rank_mhz else None}
+                        for r, (w, k) in enumerate(res["per_rank"])],
+            "distinct_gpus": shard.distinct_devices(idents),
+            "rehearse_shared_gpu": bool(args.rehearse_shared_gpu),
             "parity_first_4096_vs_golden": parity,
             "digest_sample": sample,
             "digests_sha1": digests_sha1,

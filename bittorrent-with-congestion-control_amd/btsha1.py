@@ -69,6 +69,7 @@ _sig("bt_sha1_kernel_name", ctypes.c_char_p, _u64)
 _sig("bt_sha1_clock_probe", ctypes.c_int, _vp, _u64, _u64, _u64, _vp, _vp, _vp)
 _sig("bt_sha1_wallclock_khz", _i64)
 _sig("bt_sha1_debug_barrier_stats", ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int)
+_sig("bt_sha1_debug_dropin_residue", _i64, ctypes.c_int)
 _sig("bt_sha1_chunks_file", _i64, _vp, _u64, _vp, _u64)
 _sig("bt_sha1_verifier_create", _vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32)
 _sig("bt_sha1_verifier_destroy", None, _vp)
@@ -167,6 +168,13 @@ def debug_barrier_stats(reset=False):
     out = (ctypes.c_uint64 * 3)()
     _check(lib.bt_sha1_debug_barrier_stats(out, 1 if reset else 0), "bt_sha1_debug_barrier_stats")
     return tuple(int(x) for x in out)
+
+
+def debug_dropin_residue(device=0):
+    """Nonzero bytes left in the drop-in calls' pinned staging on `device`
+    (0 between calls: each shahash / SHA1Update / SHA1Final zeroes what it
+    staged, as chunk.c:48 and sha.c:165-174 leave nothing behind)."""
+    return _check(lib.bt_sha1_debug_dropin_residue(device), "bt_sha1_debug_dropin_residue")
 
 
 # ---- device-resident (addresses are ints) ------------------------------------

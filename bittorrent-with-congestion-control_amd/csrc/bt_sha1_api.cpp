@@ -493,6 +493,7 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
     return 0;
   };
   for (auto &l : c->lane) l.busy = false;
+  const size_t kept_cap[2] = {c->lane[0].d_in.cap, c->lane[1].d_in.cap};
   // When a second batch will be needed, size lane 1 on a helper thread while
   // lane 0 is filled and copied: pinning ~1 GiB costs ~0.2-0.5 s per process.
   std::thread pre;
@@ -575,10 +576,18 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   if (drain(c->lane[k & 1]) || drain(c->lane[(k + 1) & 1])) return -1;
   // Direct-DMA batches bigger than a staged batch (BT_SHA1_DMA_BATCH_MB >
   // 1024) are not kept past the call: the lanes keep at most 1 GiB of HBM
-  // each, so a process that shares the GPU does not lose more for good.
-  if (!staged)
-    for (auto &l : c->lane)
-      if (l.d_in.cap > batch_bytes_for(chunk_len, UINT64_MAX, true)) l.d_in.release();
+  // each, so a process that shares the GPU does not lose more for good.  An
+  // oversized lane goes back to what it held before the call (capped at the
+  // staged size), so the next staged call finds its kept lane in place.
+  if (!staged) {
+    const uint64_t keep = batch_bytes_for(chunk_len, UINT64_MAX, true);
+    for (int i = 0; i < 2; ++i) {
+      DevBuf &d = c->lane[i].d_in;
+      if (d.cap <= keep) continue;
+      d.release();
+      if (kept_cap[i] && d.ensure(std::min<uint64_t>(kept_cap[i], keep))) return -1;
+    }
+  }
   if (trace_on())
     fprintf(stderr, "libbtsha1 pipeline dev %d: %llu chunks, batch %llu B, %s: total %.4f s = alloc %.4f + fill %.4f "
                     "+ wait %.4f + other\n",
@@ -718,6 +727,18 @@ int wait_chain(DevCtx *c, const volatile uint32_t *done, uint32_t seq) {
 
 uint32_t *done_word(DevCtx *c) { return reinterpret_cast<uint32_t *>(c->h_state.as<uint8_t>() + 32); }
 
+// The reference leaves no copy of the message or of the chaining state behind
+// a call: shahash zeroes its context (chunk.c:48) and SHA1Update burns its
+// stack frame (sha.c:165-174, 526).  The drop-in's copies live in the
+// context's pinned staging, so each call zeroes what it staged there once the
+// chain kernel has finished with it (explicit_bzero: not elided as a dead
+// store).  The completion word at h_state + 32 is a sequence number, not data.
+constexpr size_t kStateBytes = 32;
+void wipe_staging(DevCtx *c, size_t msg_bytes) {
+  if (msg_bytes) explicit_bzero(c->h_msg.p, std::min(msg_bytes, c->h_msg.cap));
+  explicit_bzero(c->h_state.p, kStateBytes);
+}
+
 // Single message on the GPU (shahash): copy it into the context's pinned
 // staging buffer and launch the chain kernel on it there -- the kernel reads
 // the message over PCIe itself (64 blocks per load batch, far ahead of the
@@ -730,10 +751,12 @@ int hash_one(DevCtx *c, const uint8_t *buf, uint32_t len, uint8_t out[20]) {
   if (len) memcpy(c->h_msg.p, buf, len);
   const uint32_t seq = ++c->seq;
   *done_word(c) = seq - 1u;
-  BT_CK(btsha1_launch_chain_one(c->h_msg.p, len, c->h_state.as<uint8_t>(), c->s, done_word(c), seq));
-  if (wait_chain(c, done_word(c), seq)) return -1;
-  memcpy(out, c->h_state.p, 20);
-  return 0;
+  const hipError_t e = btsha1_launch_chain_one(c->h_msg.p, len, c->h_state.as<uint8_t>(), c->s, done_word(c), seq);
+  if (e != hipSuccess) set_err("chain kernel launch: %s", hipGetErrorString(e));
+  const int rc = e != hipSuccess ? -1 : wait_chain(c, done_word(c), seq);
+  if (!rc) memcpy(out, c->h_state.p, 20);
+  wipe_staging(c, len);
+  return rc;
 }
 
 // Advance h over `head` (0 or 64 bytes: SHA1Update's completed staging block)
@@ -752,10 +775,13 @@ int midstate(DevCtx *c, uint32_t h[5], const uint8_t *head, const uint8_t *block
   nblocks = total;
   const uint32_t seq = ++c->seq;
   *done_word(c) = seq - 1u;
-  BT_CK(btsha1_launch_chain_midstate(c->h_state.as<uint32_t>(), c->h_msg.p, nblocks, c->s, done_word(c), seq));
-  if (wait_chain(c, done_word(c), seq)) return -1;
-  memcpy(h, c->h_state.p, 20);
-  return 0;
+  const hipError_t e = btsha1_launch_chain_midstate(c->h_state.as<uint32_t>(), c->h_msg.p, nblocks, c->s,
+                                                    done_word(c), seq);
+  if (e != hipSuccess) set_err("chain kernel launch: %s", hipGetErrorString(e));
+  const int rc = e != hipSuccess ? -1 : wait_chain(c, done_word(c), seq);
+  if (!rc) memcpy(h, c->h_state.p, 20);
+  wipe_staging(c, (size_t)total * 64);
+  return rc;
 }
 
 DevCtx *dropin_ctx(const char *who) {
@@ -868,6 +894,26 @@ int bt_sha1_debug_barrier_stats(uint64_t out[3], int reset) {
   }
   BT_CK(e);
   return 0;
+}
+
+int64_t bt_sha1_debug_dropin_residue(int device) {
+  DevCtx *c = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    if (device < 0) {
+      set_err("device %d out of range", device);
+      return -1;
+    }
+    if (device < (int)g_ctx.size()) c = g_ctx[device].get();
+  }
+  if (!c) return 0;  // no drop-in call has run on this device: nothing staged
+  std::lock_guard<std::mutex> g(c->mu);
+  int64_t nz = 0;
+  const uint8_t *m = c->h_msg.as<uint8_t>();
+  for (size_t i = 0; m && i < c->h_msg.cap; ++i) nz += m[i] != 0;
+  const uint8_t *st = c->h_state.as<uint8_t>();
+  for (size_t i = 0; st && i < kStateBytes; ++i) nz += st[i] != 0;
+  return nz;
 }
 
 int bt_sha1_set_variant(int nbuf, int lines, int nt) {
@@ -1230,6 +1276,7 @@ void SHA1Final(SHA1Context *sc, uint8_t hash[SHA1_HASH_SIZE]) {
     std::lock_guard<std::mutex> g(c->mu);
     if (midstate(c, sc->hash, nullptr, blk, end / 64u)) die("SHA1Final");
   }
+  explicit_bzero(blk, sizeof blk);  // the message tail (sha.c:165-174's burnStack)
   sc->totalLength += (uint64_t)(npad + 8u) * 8u;
   sc->bufferLength = 0;
   if (hash)

@@ -67,26 +67,42 @@ def gather_objects(obj, world, group=None):
     return out
 
 
-def check_distinct_devices(idents, world):
-    """The N > 1 line must come from N distinct GPUs.  `idents` is every
-    rank's {"rank", "pci_bdf", "device_count", ...}.  When each rank can see at
-    least `world` devices (a full node: rank r drives device r), two ranks on
-    one PCI address is a launch error -> the message; otherwise None.  With
-    fewer visible devices than ranks (the one-GPU rehearsal, or one device per
-    rank through *_VISIBLE_DEVICES) ranks may share a device by design and
-    the guard stays off; the line still records every rank's address."""
-    if world <= 1 or len(idents) != world:
+def device_key(ident):
+    """One physical GPU: (host, PCI address, UUID).  The host keeps two nodes'
+    equal PCI addresses apart (a multi-node launch); the UUID can only split
+    keys further (never merge two GPUs), e.g. partitions behind one address."""
+    return (ident.get("host"), ident.get("pci_bdf"), ident.get("uuid"))
+
+
+def distinct_devices(idents):
+    """How many distinct GPUs the ranks drove (bench.py's `distinct_gpus`)."""
+    return len({device_key(i) for i in idents})
+
+
+def check_distinct_devices(idents, world, allow_shared=False):
+    """An N-GPU line must come from N distinct GPUs.  `idents` is every rank's
+    {"rank", "host", "pci_bdf", "uuid", ...}.  Returns a message (every rank
+    then exits before the timed region) when fewer than `world` distinct GPUs
+    drive the ranks -- whatever each rank's device_count says: one device
+    visible per rank (*_VISIBLE_DEVICES) is fine as long as the devices
+    differ -- or when the gather is incomplete; None when the launch is sound.
+    allow_shared (bench.py --rehearse-shared-gpu, recorded in the line) lets
+    ranks share GPUs on purpose: the rank path rehearsed on one GPU."""
+    if world <= 1:
         return None
-    if min(int(i.get("device_count") or 0) for i in idents) < world:
+    if len(idents) != world:
+        return f"identity gather returned {len(idents)} of {world} ranks"
+    if allow_shared:
         return None
     seen = {}
     for i in idents:
-        seen.setdefault(i.get("pci_bdf"), []).append(i.get("rank"))
-    dup = {bdf: ranks for bdf, ranks in seen.items() if len(ranks) > 1}
-    if dup:
-        return (f"{world} ranks see >= {world} devices each, but ranks share a GPU: "
-                + ", ".join(f"{bdf} <- ranks {ranks}" for bdf, ranks in sorted(dup.items(), key=str)))
-    return None
+        seen.setdefault(device_key(i), []).append(i.get("rank"))
+    if len(seen) == world:
+        return None
+    dup = {k: ranks for k, ranks in seen.items() if len(ranks) > 1}
+    return (f"{world} ranks but {len(seen)} distinct GPU(s): ranks share a GPU ("
+            + ", ".join(f"{k[1]} on {k[0]} <- ranks {ranks}" for k, ranks in sorted(dup.items(), key=str))
+            + "); pass --rehearse-shared-gpu to run the rank path on shared GPUs on purpose")
 
 
 def gather_digests(local: bytes, world, rank, group=None):

@@ -107,6 +107,15 @@ int64_t bt_sha1_wallclock_khz(void);
  * library, which counts nothing. */
 int bt_sha1_debug_barrier_stats(uint64_t out[3], int reset);
 
+/* Diagnostic: bytes still nonzero in the pinned staging the drop-in calls
+ * (shahash, SHA1Update, SHA1Final) copy the message and the chaining state
+ * into on `device` -- every call zeroes what it staged before it returns, as
+ * the reference leaves no copy behind (chunk.c:48; sha.c:165-174, 526), so
+ * this is 0 between calls.  0 when no drop-in call has run on the device;
+ * -1 for a negative device.  Scans the whole staging buffer: a test hook, not
+ * for hot loops. */
+int64_t bt_sha1_debug_dropin_residue(int device);
+
 /* ---- device-resident batches (the hot path) ---------------------------- */
 /* n chunks of chunk_len bytes, chunk i at d_in + i*pitch (pitch >= chunk_len).
  * d_digests receives 20*n bytes, digest i = SHA-1(chunk i) as sha.c:545-556
@@ -138,9 +147,12 @@ int bt_sha1_host_unregister(void *h_ptr);
  * page-locked host memory (pageable input) and 2 x 1 GiB of HBM.  Pinned or
  * registered input is DMA'd straight from the caller's memory into the same
  * HBM lanes (1 GiB batches).  With BT_SHA1_DMA_BATCH_MB above 1024 the
- * direct-DMA batches are bigger and freed before the call returns; freeing
- * them (hipFree) synchronises the whole device, so such a call returns only
- * after work other streams of this process queued on the GPU has finished. */
+ * direct-DMA batches are bigger; before the call returns each oversized lane
+ * is freed and re-allocated at the size it had before the call (at most the
+ * 1 GiB kept lane), so the call leaves exactly the kept lanes allocated.
+ * Freeing (hipFree) synchronises the whole device, so such a call returns
+ * only after work other streams of this process queued on the GPU has
+ * finished. */
 int64_t bt_sha1_chunks_host(const void *h_in, uint64_t total_len, uint64_t chunk_len,
                             uint8_t *h_digests);
 /* The same split over the first `ndev` GPUs (<=0: all), one host thread per

@@ -115,18 +115,22 @@ int main(void) {
   /* thread creation refused (RLIMIT_NPROC in a child, as an unprivileged
    * user): both batch drivers return -1 after joining only the threads that
    * started, instead of joining unset handles or reporting partial output. */
+  /* Where root cannot drop to uid 65534 (unmapped in a user namespace, or
+   * setuid not permitted) the limit would not bind: the check is skipped. */
   fflush(stdout);
   pid_t pid = fork();
   if (pid == 0) {
-    if (geteuid() == 0 && (setgid(65534) || setuid(65534))) _exit(3);
+    if (geteuid() == 0 && (setgid(65534) || setuid(65534))) _exit(7);
     struct rlimit one = {1, 1};
-    if (setrlimit(RLIMIT_NPROC, &one)) _exit(4);
+    if (setrlimit(RLIMIT_NPROC, &one)) _exit(7);
     const int rh = or_hash_chunks(img, n, L, L, 999, b, 8);
     const int rs = or_synth_digests(first, m, L, 77, c2, 8);
     _exit(rh == -1 && rs == -1 ? 0 : 5);
   }
   int st = 0;
-  if (pid < 0 || waitpid(pid, &st, 0) != pid || !WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+  if (pid > 0 && waitpid(pid, &st, 0) == pid && WIFEXITED(st) && WEXITSTATUS(st) == 7) {
+    puts("skip thread-creation check: cannot drop to an unprivileged user here");
+  } else if (pid < 0 || !WIFEXITED(st) || WEXITSTATUS(st) != 0) {
     printf("FAIL thread-creation failure not reported cleanly (status %d)\n", st);
     fails++;
   }

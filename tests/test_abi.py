@@ -91,6 +91,16 @@ def test_barrier_tallies_only_in_the_debug_build():
     assert b"g_bar_stats" not in open(LIB, "rb").read()
 
 
+def test_dropin_residue_hook_needs_no_device():
+    """bt_sha1_debug_dropin_residue (the wipe-contract probe, chunk.c:48):
+    nothing staged before any drop-in call -> 0, a negative device -> -1,
+    with no HIP call made (the GPU tests check it reads 0 after real calls)."""
+    bt = load_btsha1()
+    assert bt.debug_dropin_residue(0) == 0
+    with pytest.raises(bt.BtSha1Error, match="out of range"):
+        bt.debug_dropin_residue(-1)
+
+
 EXP_LIB = os.path.join(REPO, "build_variants", "experiments", "libbtsha1.so")
 
 

@@ -1,6 +1,8 @@
 """GPU: bench.py's own multi-rank path, launched exactly as the driver launches
 it for N > 1 (torch.distributed.run, one process per rank, 127.0.0.1
-rendezvous), with every rank on this box's one MI355X (8 ranks = the driver's N = 8 line).
+rendezvous) and as a plain `python bench.py --gpus N` (bench.py then starts
+the ranks itself), with every rank on this box's one MI355X (8 ranks = the
+driver's N = 8 line) under --rehearse-shared-gpu -- and refused without it.
 
 What runs is the code the 8-GPU scaling bench runs: DeviceHasher per rank
 (device generator over the rank's GLOBAL chunk range, one launch per step of the
@@ -42,13 +44,24 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_bench(world, chunks, *extra, timeout=240):
+def _run_bench(world, chunks, *extra, timeout=240, launcher=True, shared=True):
+    """bench.py at `world` ranks on this box's one GPU: launched the driver's
+    N > 1 way (torch.distributed.run) or, launcher=False, as the plain
+    `python bench.py --gpus N` the driver may also run (bench.py starts the
+    ranks itself).  All ranks share the one GPU, so the run needs
+    --rehearse-shared-gpu (shared=True); without it bench.py must refuse."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(REPO, "bench.py"), "--gpus", str(world), "--chunks", str(chunks),
-           "--steps", "3", "--warmup", "1", *extra]
+    env.pop("WORLD_SIZE", None)
+    args = [os.path.join(REPO, "bench.py"), "--gpus", str(world), "--chunks", str(chunks),
+            "--steps", "3", "--warmup", "1", *extra] + (["--rehearse-shared-gpu"] if shared else [])
+    if launcher:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    else:
+        cmd = [sys.executable] + args
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
+    if not shared:
+        return r
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]  # rank 0 alone prints the line
@@ -56,21 +69,22 @@ def _run_bench(world, chunks, *extra, timeout=240):
 
 
 def _check_identity(line, world, chunks):
-    """Every per_gpu entry says which GPU the rank drove (PCI address, UUID,
-    devices visible), which kernel it ran and on which global chunks.  All
-    ranks share this box's one GPU, so the addresses are equal and the
-    distinct-device guard stays off (device_count 1 < world)."""
+    """Every per_gpu entry says which GPU the rank drove (host, PCI address,
+    UUID, devices visible), which kernel it ran and on which global chunks.
+    All ranks share this box's one GPU, so the identities are equal, and the
+    line says the rank path was rehearsed on a shared GPU on purpose."""
     per = line["per_gpu"]
     assert [p["rank"] for p in per] == list(range(world))
     for r, p in enumerate(per):
-        for k in ("pci_bdf", "uuid", "device_count", "hip_device", "kernel", "chunk_range"):
+        for k in ("host", "pci_bdf", "uuid", "device_count", "hip_device", "kernel", "chunk_range"):
             assert k in p, (k, p)
         assert p["kernel"] == line["roofline"]["kernel"]
         assert p["chunk_range"] == [r * chunks, (r + 1) * chunks]
         assert p["device_count"] >= 1 and len(p["pci_bdf"].split(":")) == 3
-    assert len({p["pci_bdf"] for p in per}) == line["distinct_gpus"]
+    assert len({(p["host"], p["pci_bdf"], p["uuid"]) for p in per}) == line["distinct_gpus"]
     if per[0]["device_count"] < world:
         assert line["distinct_gpus"] == 1 and len({p["uuid"] for p in per}) == 1
+    assert line["rehearse_shared_gpu"] is (world > 1)
 
 
 def _check_sample(line, world, chunks, oracle):
@@ -126,6 +140,44 @@ def test_bench_ranks_run_the_hot_kernel_with_parity_on_every_rank(oracle, world,
     assert [p["rank"] for p in line["per_gpu"]] == list(range(world))
     _check_identity(line, world, chunks)
     _check_sample(line, world, chunks, oracle)
+    _check_rank_clocks(line, world)
+
+
+def _check_rank_clocks(line, world):
+    """Every rank stamped its own in-kernel clock after the timed region; the
+    VALU roofline is priced at the slowest rank's."""
+    mhz = [p["in_kernel_mhz"] for p in line["per_gpu"]]
+    assert all(m is not None and 300 < m < 3000 for m in mhz), mhz
+    clock = line["clock"]
+    assert clock["in_kernel_mhz"] == min(mhz) and clock["probe_digests_identical"] is True
+    assert clock["per_rank_mhz"] == mhz and mhz[clock["slowest_rank"]] == min(mhz)
+    v = line["valu_roofline"]
+    assert abs(v["peak_at_measured_clock"] - v["peak"] * min(mhz) / 2400.0) < 0.02 * v["peak"]
+
+
+def test_bench_gpus_flag_alone_starts_the_ranks(oracle):
+    """`python3 bench.py --gpus 2` with no launcher (the driver's BENCH command
+    shape): bench.py starts the two ranks itself and relays rank 0's one line
+    -- n_gpus 2, two per_gpu entries, every digest equal to the reference's
+    checksum for 81,920 chunks, per-rank clocks."""
+    chunks = 40960
+    line = _run_bench(2, chunks, "--power-s", "0", launcher=False, timeout=300)
+    assert line["n_gpus"] == 2 and len(line["per_gpu"]) == 2
+    assert line["config"]["global_chunks"] == 2 * chunks
+    assert line["parity_all_vs_golden"] is True and line["parity_first_4096_vs_golden"] is True
+    _check_identity(line, 2, chunks)
+    _check_rank_clocks(line, 2)
+
+
+@pytest.mark.parametrize("launcher", [True, False])
+def test_bench_refuses_ranks_sharing_a_gpu_without_the_rehearsal_flag(launcher):
+    """Two ranks on this box's one GPU without --rehearse-shared-gpu: every
+    rank exits before the timed region (a line claiming 2 GPUs on 1 is never
+    printed), whichever way the ranks were started."""
+    r = _run_bench(2, 512, "--power-s", "0", "--no-clock", launcher=launcher, shared=False, timeout=240)
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "distinct GPU" in r.stderr and "--rehearse-shared-gpu" in r.stderr
 
 
 def test_bench_single_rank_line_checks(oracle):
@@ -147,4 +199,10 @@ def test_bench_single_rank_line_checks(oracle):
     assert 0 < line["bench_wall_s"] < 600 and line["phases_s"]["warmup_and_timed_s"] > 0
     v = line["verify_dev"]
     assert v["flags_correct"] is True and v["mismatches_planted"] == len(range(0, 4096, 997)) and v["GiB_per_s"] > 0
+    # the fused compare, timed paired with the plain hash in one window
+    assert v["hash_ms"] > 0 and v["verify_ms"] > 0 and v["pairs"] >= 5
+    assert abs(v["overhead_pct"] - 100.0 * (v["verify_ms"] / v["hash_ms"] - 1.0)) < 0.01
+    o = v["overhead_pct_pairs"]
+    assert o["min"] <= o["median"] <= o["max"]
+    assert line["rehearse_shared_gpu"] is False and line["distinct_gpus"] == 1
     _check_sample(line, 1, 4096, oracle)

@@ -52,6 +52,29 @@ def test_shahash_kats(bt):
     data = kat_data()
     for name, n, h in read_pairs("kat.txt"):
         assert bt.shahash(data[name]).hex() == h, name
+        # chunk.c:48: nothing of the message or the state is left behind
+        assert bt.debug_dropin_residue(0) == 0, name
+
+
+def test_dropin_calls_leave_no_staged_message_behind(bt, oracle):
+    """The reference's wipe contract (chunk.c:48 zeroes shahash's context;
+    sha.c:165-174, 526 burn SHA1Update's stack): after every drop-in call the
+    pinned staging that held the caller's message and the chaining state reads
+    all zero -- a 512 KiB chunk of nonzero bytes through shahash, and a
+    streaming SHA1Update / SHA1Final sequence -- and the digests are still
+    bit-exact."""
+    chunk = bytes(oracle.fill_synthetic(512 * 1024, 99, 0x51A7))
+    assert chunk.count(0) < len(chunk) // 100
+    assert bt.shahash(chunk) == oracle.sha1(chunk)
+    assert bt.debug_dropin_residue(0) == 0
+    s = bt.Sha1()
+    for a, b in ((0, 100), (100, 64 * 1000 + 7), (64 * 1000 + 7, len(chunk))):
+        s.update(chunk[a:b])
+        assert bt.debug_dropin_residue(0) == 0, (a, b)
+    assert s.final() == oracle.sha1(chunk)
+    assert bt.debug_dropin_residue(0) == 0
+    with pytest.raises(bt.BtSha1Error):
+        bt.debug_dropin_residue(-1)
 
 
 def test_shahash_either_side_of_the_hot_kernel_limit(bt, oracle):

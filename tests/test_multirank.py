@@ -119,43 +119,48 @@ def test_bench_rank_protocol_two_ranks(oracle):
     assert nranks == 2 and abs(kmax - 1.006) < 1e-9
 
 
-def _ident_worker(rank, world, port, shared, q):
+def _ident_worker(rank, world, port, shared, allow, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     shard = _load_shard()
     bdf = "0000:05:00.0" if shared else f"0000:{0x05 + 0x10 * rank:02x}:00.0"
-    ident = {"rank": rank, "pci_bdf": bdf, "uuid": f"stub-{rank}", "device_count": world,
+    # shared: the one-GPU box (device_count 1, one PCI address for both ranks)
+    ident = {"rank": rank, "host": "box", "pci_bdf": bdf, "uuid": "stub-0" if shared else f"stub-{rank}",
+             "device_count": 1 if shared else world,
              "kernel": "k_sha1_fixed", "chunk_range": list(shard.weak_range(rank, 131072))}
     idents = shard.gather_objects(ident, world)
-    q.put((rank, idents, shard.check_distinct_devices(idents, world)))
+    q.put((rank, idents, shard.check_distinct_devices(idents, world, allow_shared=allow),
+           shard.distinct_devices(idents)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("shared", [False, True])
-def test_rank_identities_gathered_and_shared_gpu_refused(shared):
+@pytest.mark.parametrize("shared,allow", [(False, False), (True, False), (True, True)])
+def test_rank_identities_gathered_and_shared_gpu_refused(shared, allow):
     """bench.py's pre-timing identity exchange at world size 2 (gloo): every
-    rank gets every rank's {PCI address, UUID, devices visible, kernel, chunk
-    range} in rank order, and when each rank sees >= world devices yet two
-    ranks report one PCI address, EVERY rank gets the clash (so all exit
-    before the timed region); stub identities stand in for the GPUs."""
+    rank gets every rank's {host, PCI address, UUID, devices visible, kernel,
+    chunk range} in rank order.  Two ranks on one GPU -- here a stub pair on
+    one PCI address with device_count 1, the shape of a one-GPU box -- give
+    EVERY rank the clash (all exit before the timed region) unless the launch
+    asked for a shared-GPU rehearsal (--rehearse-shared-gpu)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ident_worker, args=(r, world, port, shared, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ident_worker, args=(r, world, port, shared, allow, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, idents, clash in got:
+    for rank, idents, clash, distinct in got:
         assert [i["rank"] for i in idents] == [0, 1]
         assert [i["chunk_range"] for i in idents] == [[0, 131072], [131072, 262144]]
-        if shared:
-            assert clash and "0000:05:00.0 <- ranks [0, 1]" in clash
+        assert distinct == (1 if shared else 2)
+        if shared and not allow:
+            assert clash and "0000:05:00.0 on box <- ranks [0, 1]" in clash and "--rehearse-shared-gpu" in clash
         else:
             assert clash is None
 
@@ -163,17 +168,27 @@ def test_rank_identities_gathered_and_shared_gpu_refused(shared):
 def test_distinct_device_guard_logic():
     shard = _load_shard()
 
-    def ids(bdfs, count):
-        return [{"rank": r, "pci_bdf": b, "device_count": count} for r, b in enumerate(bdfs)]
+    def ids(bdfs, count, hosts=None):
+        return [{"rank": r, "host": (hosts or ["n0"] * len(bdfs))[r], "pci_bdf": b, "uuid": None,
+                 "device_count": count} for r, b in enumerate(bdfs)]
     full = [f"0000:{b:02x}:00.0" for b in (0x05, 0x15, 0x65, 0x75, 0x85, 0x95, 0xe5, 0xf5)]
     assert shard.check_distinct_devices(ids(full, 8), 8) is None            # a full node, one GPU per rank
+    assert shard.check_distinct_devices(ids(full, 1), 8) is None            # one visible device per rank, distinct
     bad = full[:7] + [full[3]]
     msg = shard.check_distinct_devices(ids(bad, 8), 8)
-    assert msg and "ranks [3, 7]" in msg                                     # two ranks on one GPU
-    assert shard.check_distinct_devices(ids([full[0]] * 8, 1), 8) is None   # one-GPU rehearsal: guard off
-    assert shard.check_distinct_devices(ids([full[0]] * 2, 1), 2) is None
-    assert shard.check_distinct_devices(ids(full[:4], 4), 8) is None        # incomplete gather: no verdict
+    assert msg and "ranks [3, 7]" in msg and "7 distinct" in msg            # two ranks on one GPU
+    assert shard.check_distinct_devices(ids(bad, 1), 8)                     # ... whatever device_count says
+    assert shard.check_distinct_devices(ids([full[0]] * 8, 1), 8)           # one-GPU box: refused by default
+    assert shard.check_distinct_devices(ids([full[0]] * 8, 1), 8, allow_shared=True) is None  # the rehearsal
+    assert shard.check_distinct_devices(ids([full[0]] * 2, 1), 2)
+    assert "4 of 8" in shard.check_distinct_devices(ids(full[:4], 4), 8)    # incomplete gather
     assert shard.check_distinct_devices(ids(full[:1], 8), 1) is None        # N = 1
+    # two nodes x 4 ranks: equal PCI addresses on different hosts are different GPUs
+    two = ids(full[:4] * 2, 8, hosts=["n0"] * 4 + ["n1"] * 4)
+    assert shard.check_distinct_devices(two, 8) is None and shard.distinct_devices(two) == 8
+    # UUIDs only split keys: same address + host but different UUIDs -> distinct
+    parts = [{"rank": r, "host": "n0", "pci_bdf": full[0], "uuid": f"u{r}"} for r in range(2)]
+    assert shard.check_distinct_devices(parts, 2) is None
 
 
 def test_bench_uses_the_shard_protocol():

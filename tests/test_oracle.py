@@ -206,13 +206,19 @@ n, L = 64, 4096
 img = (ctypes.c_uint8 * (n * L))()
 out = (ctypes.c_uint8 * (20 * n))()
 ok_all = lib.or_synth_digests(0, n, L, 77, out, 8)       # unrestricted: 0
-if os.geteuid() == 0:
-    os.setgid(65534)
-    os.setuid(65534)
-resource.setrlimit(resource.RLIMIT_NPROC, (1, 1))
+try:
+    if os.geteuid() == 0:
+        os.setgid(65534)
+        os.setuid(65534)
+    resource.setrlimit(resource.RLIMIT_NPROC, (1, 1))
+except OSError as e:  # uid 65534 unmapped / setuid not permitted: the limit would not bind
+    print("SKIP", e)
+    sys.exit(0)
 print(ok_all, lib.or_synth_digests(0, n, L, 77, out, 8), lib.or_hash_chunks(img, n, L, L, L, out, 16))
 '''
     r = subprocess.run([sys.executable, "-c", code, f"{REPO}/oracle/liboracle_sha1.so"],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
+    if r.stdout.startswith("SKIP"):
+        pytest.skip(f"cannot drop to an unprivileged user here: {r.stdout.strip()}")
     assert r.stdout.split() == ["0", "-1", "-1"], r.stdout

@@ -79,9 +79,11 @@ for step in "$@"; do
     dist2)
       # the driver's N>1 launch line, rehearsed with 2 and 4 ranks sharing this box's one GPU
       run dist2 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-        --master-port 29531 bench.py --gpus 2 --chunks 16384 --steps 5 --warmup 2
+        --master-port 29531 bench.py --gpus 2 --chunks 16384 --steps 5 --warmup 2 --rehearse-shared-gpu
       run dist4 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
-        --master-port 29532 bench.py --gpus 4 --chunks 8192 --steps 5 --warmup 2 ;;
+        --master-port 29532 bench.py --gpus 4 --chunks 8192 --steps 5 --warmup 2 --rehearse-shared-gpu
+      # the driver's other N > 1 shape: no launcher, bench.py starts the ranks itself
+      run dist2_self 600 python3 bench.py --gpus 2 --chunks 16384 --steps 5 --warmup 2 --rehearse-shared-gpu ;;
     pairing)
       run pairing 300 "$ROOT/tools/ubench/pairing"
       mkdir -p "$OUT/pairing_pmc"
@@ -117,7 +119,7 @@ for step in "$@"; do
       for rep in 1 2; do
         run "occ_n1_$rep" 200 $B && run "occ_n1_262k_$rep" 200 $B --chunks 262144 && \
         run "occ_n2_$rep" 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-          --master-port 2955$rep bench.py --gpus 2 --steps 20 --warmup 5 || exit 1
+          --master-port 2955$rep bench.py --gpus 2 --steps 20 --warmup 5 --rehearse-shared-gpu || exit 1
       done ;;
     counters) run counters 120 rocprofv3 -L ;;
     residency) run residency 300 "$ROOT/tools/ubench/residency" ;;

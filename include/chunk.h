@@ -23,7 +23,11 @@ extern "C" {
  * reference documents -1 but never returns it; here a GPU error does). */
 int make_chunks(FILE *fp, uint8_t **chunk_hashes);
 
-/* chunk.h:28 -- SHA-1 of len bytes into target[20]. */
+/* chunk.h:28 -- SHA-1 of len bytes into target[20], computed on the GPU by
+ * one synchronous chain-kernel call.  Like the reference, which zeroes its
+ * context before returning (chunk.c:48), it leaves no copy of the message or
+ * of the chaining state behind: the pinned staging the kernel read them from
+ * is zeroed before the call returns. */
 void shahash(uint8_t *chr, int len, uint8_t *target);
 
 /* chunk.h:31 -- lowercase hex, NUL-terminated (ascii holds 2*len+1). */

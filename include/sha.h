@@ -36,7 +36,11 @@ extern "C" {
 
 /* sha.h:58 -- reset to the FIPS 180-1 IV. */
 void SHA1Init(SHA1Context *sc);
-/* sha.h:59 -- absorb len bytes (whole blocks are compressed on the GPU). */
+/* sha.h:59 -- absorb len bytes (whole blocks are compressed on the GPU).
+ * The reference burns its stack frame after each call (sha.c:165-174, 526);
+ * here the pinned staging the GPU read the blocks and state from is zeroed
+ * before SHA1Update / SHA1Final return (the context itself, as in the
+ * reference, keeps the partial block until the caller clears it). */
 void SHA1Update(SHA1Context *sc, const void *data, uint32_t len);
 /* sha.h:60 -- MD-pad, compress the last block(s), write the big-endian digest
  * (hash may be NULL, as in sha.c:545). */

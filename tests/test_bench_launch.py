@@ -110,3 +110,48 @@ def test_gpus_n_starts_n_ranks_through_torchrun():
     if r.returncode == 0:
         pytest.skip("a GPU is visible here; the GPU test runs this path")
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_relay_forwards_sigterm_and_the_ranks_die_with_it(tmp_path):
+    """SIGTERM to bench.py's launcher reaches the rank launch (the driver's
+    time limit, or a kill of the process it started), and the child exits
+    with it instead of running on orphaned on the GPUs."""
+    import signal
+    import time
+    pidfile = tmp_path / "child.pid"
+    child = ("import os, sys, time\n"
+             f"open({str(pidfile)!r}, 'w').write(str(os.getpid()))\n"
+             "print('rank started', flush=True)\n"
+             "time.sleep(120)\n")
+    runner = ("import importlib.util, sys\n"
+              f"spec = importlib.util.spec_from_file_location('b', {BENCH!r})\n"
+              "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
+              f"sys.exit(b.relay([sys.executable, '-c', {child!r}]))\n")
+    p = subprocess.Popen([sys.executable, "-c", runner], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    t0 = time.time()
+    while not pidfile.exists() and time.time() - t0 < 60:
+        time.sleep(0.05)
+    assert pidfile.exists(), p.stderr.read() if p.poll() is not None else "child never started"
+    cpid = int(pidfile.read_text())
+    p.send_signal(signal.SIGTERM)
+    rc = p.wait(timeout=60)
+    assert rc != 0  # the child's SIGTERM death is the launcher's status (negative: killed by signal)
+    with pytest.raises(ProcessLookupError):
+        for _ in range(100):
+            os.kill(cpid, 0)
+            time.sleep(0.05)
+
+
+def test_ensure_built_adds_the_experiments_library_only_for_variants(monkeypatch):
+    """A non-default --ring/--lines/--nt loads build_variants/experiments:
+    ensure_built must build it on a checkout that lacks it, and
+    must not build it for the default kernel."""
+    b = _bench()
+    calls = []
+    real_exists = os.path.exists
+    monkeypatch.setattr(b.subprocess, "run", lambda cmd, check: calls.append(cmd))
+    monkeypatch.setattr(b.os.path, "exists", lambda p: p != b.EXPERIMENTS_LIB and real_exists(p))
+    b.ensure_built()
+    assert calls == []
+    b.ensure_built(experiments=True)
+    assert len(calls) == 1 and calls[0][-1] == "experiments" and "lib" in calls[0]

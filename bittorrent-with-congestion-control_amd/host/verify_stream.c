@@ -2,7 +2,8 @@
  * verify-stream -- the received-chunk verify path of the peer (util.c:250-337)
  * driven through the batched GPU verifier, end to end from host memory.
  *
- *   verify-stream [-b batch] [-s streams] [-r rounds] [-p poll-every] [-x] [-z] <data-file> <chunks-file>
+ *   verify-stream [-b batch] [-s streams] [-r rounds] [-p poll-every] [-g verifiers] [-x] [-z]
+ *                 <data-file> <chunks-file>
  *
  * For every chunk listed in <chunks-file> ("<id> <hex>" lines, as
  * parse_has_get_chunk_file reads them, util.c:90-93) the chunk's bytes are
@@ -17,8 +18,10 @@
  * into bt_sha1_verifier_slot() + offset): slots are written once, then every
  * later commit re-verifies the bytes already resident in its slot, so the
  * measured rate is the H2D + hash + D2H pipeline alone.  -p N polls for
- * verdicts after every N-th commit (default 1: after each chunk).  The last line is a
- * JSON summary with the host->verdict rate.
+ * verdicts after every N-th commit (default 1: after each chunk).  -g G runs G
+ * verifiers, verifier g on device g % (visible devices), and deals received
+ * chunk `id` to verifier id % G, chunks arriving interleaved
+ * across them.  The last line is a JSON summary with the host->verdict rate.
  */
 #include <fcntl.h>
 #include <stdio.h>
@@ -87,22 +90,49 @@ static double now(void) {
   return ts.tv_sec + 1e-9 * ts.tv_nsec;
 }
 
+/* One verifier and the chunks routed to it (-g: chunk id modulo G). */
+struct lane {
+  bt_sha1_verifier *v;
+  int *ks;              /* indices into ids[] / exp[] of this verifier's chunks */
+  int nk;
+  long per_round;       /* commits per round */
+  struct resident *res; /* -z: which chunk each of its pinned slots holds */
+  long nres;
+};
+
+static int drain_all(struct lane *L, int G, long *good, long *bad, int wait) {
+  bt_sha1_verdict out[256];
+  for (int g = 0; g < G; g++) {
+    int m;
+    while ((m = wait ? bt_sha1_verifier_drain(L[g].v, out, 256) : bt_sha1_verifier_poll(L[g].v, out, 256)) > 0)
+      count(out, m, good, bad);
+    if (m < 0) {
+      fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
+      return -1;
+    }
+  }
+  return 0;
+}
+
+#define USAGE "usage: %s [-b batch] [-s streams] [-r rounds] [-p poll-every] [-g verifiers] [-x] [-z] <data-file> <chunks-file>\n"
+
 int main(int argc, char **argv) {
-  int batch = 64, streams = 2, rounds = 1, corrupt = 0, zcopy = 0, poll_every = 1, opt;
-  while ((opt = getopt(argc, argv, "b:s:r:p:xz")) != -1) {
+  int batch = 64, streams = 2, rounds = 1, corrupt = 0, zcopy = 0, poll_every = 1, G = 1, opt;
+  while ((opt = getopt(argc, argv, "b:s:r:p:g:xz")) != -1) {
     if (opt == 'b') batch = atoi(optarg);
     else if (opt == 's') streams = atoi(optarg);
     else if (opt == 'r') rounds = atoi(optarg);
     else if (opt == 'x') corrupt = 1;
     else if (opt == 'z') zcopy = 1;
     else if (opt == 'p') poll_every = atoi(optarg) > 0 ? atoi(optarg) : 1;
+    else if (opt == 'g') G = atoi(optarg);
     else {
-      fprintf(stderr, "usage: %s [-b batch] [-s streams] [-r rounds] [-p poll-every] [-x] [-z] <data-file> <chunks-file>\n", argv[0]);
+      fprintf(stderr, USAGE, argv[0]);
       return 255;
     }
   }
-  if (argc - optind != 2) {
-    fprintf(stderr, "usage: %s [-b batch] [-s streams] [-r rounds] [-p poll-every] [-x] [-z] <data-file> <chunks-file>\n", argv[0]);
+  if (argc - optind != 2 || G < 1 || G > 64) {
+    fprintf(stderr, USAGE, argv[0]);
     return 255;
   }
   int fd = open(argv[optind], O_RDONLY);
@@ -135,94 +165,115 @@ int main(int argc, char **argv) {
   }
   fclose(cf);
 
-  bt_sha1_verifier *v = bt_sha1_verifier_create(0, BT_CHUNK_SIZE, (uint32_t)batch, (uint32_t)streams);
-  if (!v) {
-    fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
-    return 255;
-  }
   /* only whole chunks are verified (util.c:307) */
   int m0 = 0;
   for (int k = 0; k < n; k++)
-    if ((uint64_t)ids[k] * BT_CHUNK_SIZE + BT_CHUNK_SIZE <= (uint64_t)st.st_size) {
+    if (ids[k] >= 0 && (uint64_t)ids[k] * BT_CHUNK_SIZE + BT_CHUNK_SIZE <= (uint64_t)st.st_size) {
       ids[m0] = ids[k];
       memcpy(exp + 20 * m0, exp + 20 * k, 20);
       m0++;
     }
   n = m0;
+  /* -g G: G verifiers, verifier g on device g % (visible devices) -- one per
+   * GPU on a node, or G sharing one GPU -- and received chunk `id` goes to
+   * verifier id % G (received chunks dealt by index modulo G). */
+  const int ndev = bt_sha1_device_count();
+  if (ndev <= 0) {
+    fprintf(stderr, "verify-stream: no HIP device visible\n");
+    return 255;
+  }
   const long ring = (long)batch * (streams < 2 ? 2 : streams);
-  long per_round = n;
-  if (zcopy) {
-    if (n == 0 || ring % n) {
-      fprintf(stderr, "verify-stream -z: batch*streams (%ld) must be a multiple of the chunk count (%d)\n", ring, n);
+  struct lane *L = calloc((size_t)G, sizeof *L);
+  long per_round_max = 0;
+  for (int g = 0; g < G; g++) {
+    L[g].v = bt_sha1_verifier_create(g % ndev, BT_CHUNK_SIZE, (uint32_t)batch, (uint32_t)streams);
+    if (!L[g].v) {
+      fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
       return 255;
     }
-    per_round = ring;
+    L[g].ks = malloc(sizeof(int) * (n ? n : 1));
+    for (int k = 0; k < n; k++)
+      if (ids[k] % G == g) L[g].ks[L[g].nk++] = k;
+    L[g].per_round = L[g].nk;
+    if (zcopy) {
+      if (L[g].nk == 0 || ring % L[g].nk) {
+        fprintf(stderr, "verify-stream -z: batch*streams (%ld) must be a multiple of each verifier's chunk count "
+                        "(verifier %d: %d)\n", ring, g, L[g].nk);
+        return 255;
+      }
+      L[g].per_round = ring;
+      /* which chunk each pinned slot holds.  The verifier hands slots out in
+       * ring order, but after a drain it resumes at whichever batch is next,
+       * so the i-th slot of a later round is not the i-th slot of round 0:
+       * every commit is paired with the chunk actually resident in its slot. */
+      L[g].res = malloc(sizeof *L[g].res * ring);
+    }
+    if (L[g].per_round > per_round_max) per_round_max = L[g].per_round;
   }
-  /* -z: which chunk each pinned slot holds.  The verifier hands slots out in
-   * ring order, but after a drain it resumes at whichever batch is next, so
-   * the i-th slot of a later round is not the i-th slot of round 0: every
-   * commit is paired with the chunk actually resident in the slot it got. */
-  struct resident *res = NULL;
-  long nres = 0;
-  if (zcopy) res = malloc(sizeof *res * ring);
-  bt_sha1_verdict out[256];
   long good = 0, bad = 0, total = 0, timed = 0;
   double t0 = now();
   for (int r = 0; r < rounds; r++) {
     if (zcopy && r == 1 && rounds > 1) {
       /* steady state: the first round only landed the data in the slots */
-      int m;
-      while ((m = bt_sha1_verifier_drain(v, out, 256)) > 0) count(out, m, &good, &bad);
+      if (drain_all(L, G, &good, &bad, 1)) return 255;
       t0 = now();
       timed = 0;
     }
-    if (zcopy && r == 1) nres = index_resident(res, nres);
-    for (long i = 0; i < per_round; i++) {
-      int k = (int)(i % n);
-      const uint64_t off = (uint64_t)ids[k] * BT_CHUNK_SIZE;
-      uint8_t *slot = bt_sha1_verifier_slot(v);
-      if (!slot) {
-        fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
-        return 255;
-      }
-      if (zcopy && r == 0) {
-        res[nres].slot = slot;
-        res[nres].seq = nres;
-        res[nres++].k = k;
-      } else if (zcopy) {
-        struct resident key = {slot, 0, 0}, *hit = bsearch(&key, res, nres, sizeof *res, cmp_slot);
-        if (!hit) {
-          fprintf(stderr, "verify-stream: slot %p was never filled\n", (void *)slot);
+    if (zcopy && r == 1)
+      for (int g = 0; g < G; g++) L[g].nres = index_resident(L[g].res, L[g].nres);
+    /* chunks arrive interleaved across the verifiers, as downloads from
+     * several peers would */
+    for (long i = 0; i < per_round_max; i++) {
+      for (int g = 0; g < G; g++) {
+        struct lane *l = &L[g];
+        if (i >= l->per_round) continue;
+        int k = l->ks[i % l->nk];
+        const uint64_t off = (uint64_t)ids[k] * BT_CHUNK_SIZE;
+        uint8_t *slot = bt_sha1_verifier_slot(l->v);
+        if (!slot) {
+          fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
           return 255;
         }
-        k = hit->k;
-      }
-      if (!zcopy || r == 0) {
-        for (uint32_t got = 0; got < BT_CHUNK_SIZE; got += PAYLOAD) { /* save_data_packet, util.c:275 */
-          uint32_t len = BT_CHUNK_SIZE - got < PAYLOAD ? BT_CHUNK_SIZE - got : PAYLOAD;
-          memcpy(slot + got, img + off + got, len);
+        if (zcopy && r == 0) {
+          l->res[l->nres].slot = slot;
+          l->res[l->nres].seq = l->nres;
+          l->res[l->nres++].k = k;
+        } else if (zcopy) {
+          struct resident key = {slot, 0, 0}, *hit = bsearch(&key, l->res, l->nres, sizeof *l->res, cmp_slot);
+          if (!hit) {
+            fprintf(stderr, "verify-stream: slot %p was never filled\n", (void *)slot);
+            return 255;
+          }
+          k = hit->k;
         }
-        if (corrupt && k % 7 == 3) slot[k % BT_CHUNK_SIZE] ^= 0x5a;
-      }
-      if (bt_sha1_verifier_commit(v, slot, BT_CHUNK_SIZE, exp + 20 * k, (uint64_t)k)) {
-        fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
-        return 255;
-      }
-      total++;
-      timed++;
-      if (total % poll_every == 0) {
-        int m;
-        while ((m = bt_sha1_verifier_poll(v, out, 256)) > 0) count(out, m, &good, &bad);
+        if (!zcopy || r == 0) {
+          for (uint32_t got = 0; got < BT_CHUNK_SIZE; got += PAYLOAD) { /* save_data_packet, util.c:275 */
+            uint32_t len = BT_CHUNK_SIZE - got < PAYLOAD ? BT_CHUNK_SIZE - got : PAYLOAD;
+            memcpy(slot + got, img + off + got, len);
+          }
+          if (corrupt && k % 7 == 3) slot[k % BT_CHUNK_SIZE] ^= 0x5a;
+        }
+        if (bt_sha1_verifier_commit(l->v, slot, BT_CHUNK_SIZE, exp + 20 * k, (uint64_t)k)) {
+          fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
+          return 255;
+        }
+        total++;
+        timed++;
+        if (total % poll_every == 0 && drain_all(L, G, &good, &bad, 0)) return 255;
       }
     }
   }
-  int m;
-  while ((m = bt_sha1_verifier_drain(v, out, 256)) > 0) count(out, m, &good, &bad);
+  if (drain_all(L, G, &good, &bad, 1)) return 255;
   double dt = now() - t0;
-  bt_sha1_verifier_destroy(v);
-  free(res);
-  printf("{\"chunks\": %ld, \"ok\": %ld, \"failed\": %ld, \"seconds\": %.6f, \"GiB_per_s\": %.4f, \"batch\": %d, \"streams\": %d, \"poll_every\": %d, \"mode\": \"%s\"}\n",
-         total, good, bad, dt, timed * (double)BT_CHUNK_SIZE / dt / (1u << 30), batch, streams, poll_every,
-         zcopy ? "zero-copy slots" : "packetized memcpy (util.c:275)");
+  for (int g = 0; g < G; g++) {
+    bt_sha1_verifier_destroy(L[g].v);
+    free(L[g].ks);
+    free(L[g].res);
+  }
+  free(L);
+  printf("{\"chunks\": %ld, \"ok\": %ld, \"failed\": %ld, \"seconds\": %.6f, \"GiB_per_s\": %.4f, \"batch\": %d, "
+         "\"streams\": %d, \"poll_every\": %d, \"verifiers\": %d, \"devices\": %d, \"mode\": \"%s\"}\n",
+         total, good, bad, dt, timed * (double)BT_CHUNK_SIZE / dt / (1u << 30), batch, streams, poll_every, G,
+         G < ndev ? G : ndev, zcopy ? "zero-copy slots" : "packetized memcpy (util.c:275)");
   return bad && !corrupt ? 1 : 0;
 }

@@ -3,6 +3,7 @@ reference's golden vectors.  Bit-exact everywhere (integer/byte work)."""
 import contextlib
 import ctypes
 import hashlib
+import json
 import os
 import random
 import subprocess
@@ -615,6 +616,35 @@ def test_verify_stream_zero_copy_distinct_chunks(tmp_path, oracle, batch, stream
     ring = batch * max(streams, 2)
     assert r.returncode == 0, (r.stdout[-500:], r.stderr[-500:])
     assert f'"chunks": {4 * ring}, "ok": {4 * ring}, "failed": 0' in r.stdout
+
+
+@pytest.mark.parametrize("g", [2, 3])
+def test_verify_stream_chunks_dealt_modulo_g_verifiers(tmp_path, oracle, g):
+    """SURVEY.md §8e's streaming-verify split: -g G verifiers (one per GPU on
+    a node; here G sharing this box's one GPU), received chunk id -> verifier
+    id % G, chunks arriving interleaved across them.  Packetized receive with
+    every 7th chunk corrupted (-x): exactly those fail, whatever G; zero-copy
+    receive (-z): every commit of every verifier's ring verifies."""
+    exe = os.path.join(PKG, "bin", "verify-stream")
+    n = 12 * g
+    img = bytes(oracle.fill_synthetic(n * CHUNK, 11, 0xFEED))
+    p = tmp_path / "img"
+    p.write_bytes(img)
+    ck = tmp_path / "img.chunks"
+    ck.write_text("".join(f"{i} {d.hex()}\n" for i, d in enumerate(oracle.hash_chunks(img, CHUNK))))
+    r = subprocess.run([exe, "-g", str(g), "-b", "4", "-s", "2", "-x", str(p), str(ck)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout[-500:], r.stderr[-500:])
+    summary = json.loads(r.stdout.strip().splitlines()[-1])
+    bad = sum(1 for k in range(n) if k % 7 == 3)
+    assert (summary["chunks"], summary["ok"], summary["failed"], summary["verifiers"]) == (n, n - bad, bad, g)
+    assert r.stdout.count("Verification failed!") == bad
+    # zero-copy: each verifier's chunk count (12) divides its ring (4 x 3)
+    r = subprocess.run([exe, "-g", str(g), "-z", "-b", "4", "-s", "3", "-r", "3", str(p), str(ck)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout[-500:], r.stderr[-500:])
+    summary = json.loads(r.stdout.strip().splitlines()[-1])
+    assert (summary["chunks"], summary["ok"], summary["failed"]) == (3 * 12 * g, 3 * 12 * g, 0)
 
 
 def test_verifier_concurrent_downloads_out_of_order(bt):

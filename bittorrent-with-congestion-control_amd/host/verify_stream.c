@@ -204,8 +204,10 @@ int main(int argc, char **argv) {
       L[g].per_round = ring;
       /* which chunk each pinned slot holds.  The verifier hands slots out in
        * ring order, but after a drain it resumes at whichever batch is next,
-       * so the i-th slot of a later round is not the i-th slot of round 0:
-       * every commit is paired with the chunk actually resident in its slot. */
+       * and a batch harvested before the next slot request is refilled in
+       * place, so the i-th slot of a later round is not the i-th slot of
+       * round 0: every commit is paired with the chunk actually resident in
+       * its slot, and a slot first seen after round 0 is filled then. */
       L[g].res = malloc(sizeof *L[g].res * ring);
     }
     if (L[g].per_round > per_round_max) per_round_max = L[g].per_round;
@@ -227,8 +229,7 @@ int main(int argc, char **argv) {
       for (int g = 0; g < G; g++) {
         struct lane *l = &L[g];
         if (i >= l->per_round) continue;
-        int k = l->ks[i % l->nk];
-        const uint64_t off = (uint64_t)ids[k] * BT_CHUNK_SIZE;
+        int k = l->ks[i % l->nk], fill = 0;
         uint8_t *slot = bt_sha1_verifier_slot(l->v);
         if (!slot) {
           fprintf(stderr, "verify-stream: %s\n", bt_sha1_last_error());
@@ -240,13 +241,28 @@ int main(int argc, char **argv) {
           l->res[l->nres++].k = k;
         } else if (zcopy) {
           struct resident key = {slot, 0, 0}, *hit = bsearch(&key, l->res, l->nres, sizeof *l->res, cmp_slot);
-          if (!hit) {
-            fprintf(stderr, "verify-stream: slot %p was never filled\n", (void *)slot);
+          if (hit) {
+            k = hit->k;
+          } else if (l->nres < ring) {
+            /* A slot round 0 never got: a batch harvested between two slot
+             * requests is refilled in place instead of the ring advancing, so
+             * which slots round 0 touched depends on timing.  Its first use is
+             * its receive: fill it with this commit's chunk and remember it. */
+            long at = 0;
+            while (at < l->nres && l->res[at].slot < slot) at++;
+            memmove(l->res + at + 1, l->res + at, sizeof *l->res * (size_t)(l->nres - at));
+            l->res[at].slot = slot;
+            l->res[at].seq = at;
+            l->res[at].k = k;
+            l->nres++;
+            fill = 1;
+          } else {
+            fprintf(stderr, "verify-stream: more distinct slots than the ring holds (%p)\n", (void *)slot);
             return 255;
           }
-          k = hit->k;
         }
-        if (!zcopy || r == 0) {
+        if (!zcopy || r == 0 || fill) {
+          const uint64_t off = (uint64_t)ids[k] * BT_CHUNK_SIZE;
           for (uint32_t got = 0; got < BT_CHUNK_SIZE; got += PAYLOAD) { /* save_data_packet, util.c:275 */
             uint32_t len = BT_CHUNK_SIZE - got < PAYLOAD ? BT_CHUNK_SIZE - got : PAYLOAD;
             memcpy(slot + got, img + off + got, len);

@@ -921,8 +921,12 @@ def main():
             # per rank: its rate and kernel time, and which GPU it was (PCI address,
             # UUID, devices visible), which kernel it ran and on which global chunks
             "per_gpu": [{**idents[r], "GiB_per_s": round(C * CHUNK * args.steps / w / 2**30, 3),
-                         "kernel_ms": round(k, 4), "in_kernel_mhz": rank_mhz[r] if rank_mhz else None}
+                         "kernel_ms": round(k, 4), "kernel_GiB_per_s": round(C * CHUNK / (k * 1e-3) / 2**30, 3),
+                         "in_kernel_mhz": rank_mhz[r] if rank_mhz else None}
                         for r, (w, k) in enumerate(res["per_rank"])],
+            # SURVEY.md §8d config 4's aggregate: all ranks' bytes of one step /
+            # the slowest rank's average hot-kernel time (HIP events)
+            "aggregate_kernel_GiB_per_s": round(world * C * CHUNK / (kern_max * 1e-3) / 2**30, 3),
             "distinct_gpus": shard.distinct_devices(idents),
             "rehearse_shared_gpu": bool(args.rehearse_shared_gpu),
             "parity_first_4096_vs_golden": parity,

@@ -115,6 +115,12 @@ def test_bench_ranks_split_and_gather_on_one_gpu(world, oracle):
     assert line["parity_first_4096_vs_golden"] is True
     assert [p["rank"] for p in line["per_gpu"]] == list(range(world))
     assert all(p["GiB_per_s"] > 0 and p["kernel_ms"] > 0 for p in line["per_gpu"])
+    # §8d config 4's aggregate: all ranks' bytes / the slowest rank's kernel time
+    slowest = max(p["kernel_ms"] for p in line["per_gpu"])
+    assert abs(line["aggregate_kernel_GiB_per_s"] - world * chunks * CHUNK / (slowest * 1e-3) / 2**30) < \
+        1e-3 * line["aggregate_kernel_GiB_per_s"] + 0.01
+    assert all(abs(p["kernel_GiB_per_s"] * p["kernel_ms"] * 1e-3 * 2**30 - chunks * CHUNK) < 1e-3 * chunks * CHUNK
+               for p in line["per_gpu"])
     assert line["value"] > 0 and line["scaling"] == "weak"
     # N > 1: no CPU baseline / host-path legs (rank 0 at N = 1 only)
     assert line["cpu_baseline"] is None and line["host_path"] is None

@@ -161,18 +161,22 @@ def _check_rank_clocks(line, world):
     assert abs(v["peak_at_measured_clock"] - v["peak"] * min(mhz) / 2400.0) < 0.02 * v["peak"]
 
 
-def test_bench_gpus_flag_alone_starts_the_ranks(oracle):
-    """`python3 bench.py --gpus 2` with no launcher (the driver's BENCH command
-    shape): bench.py starts the two ranks itself and relays rank 0's one line
-    -- n_gpus 2, two per_gpu entries, every digest equal to the reference's
-    checksum for 81,920 chunks, per-rank clocks."""
-    chunks = 40960
-    line = _run_bench(2, chunks, "--power-s", "0", launcher=False, timeout=300)
-    assert line["n_gpus"] == 2 and len(line["per_gpu"]) == 2
-    assert line["config"]["global_chunks"] == 2 * chunks
+@pytest.mark.parametrize("world,chunks", [(2, 40960), (8, 512)])
+def test_bench_gpus_flag_alone_starts_the_ranks(oracle, world, chunks):
+    """`python3 bench.py --gpus N` with no launcher (the driver's BENCH command
+    shape): bench.py starts the N ranks itself and relays rank 0's one line
+    -- n_gpus N, N per_gpu entries, every digest equal to the reference's
+    checksum (81,920 chunks on the hot kernel with per-rank clocks; 8 ranks x
+    512 chunks = config 2's 4096 on the latency kernel)."""
+    line = _run_bench(world, chunks, "--power-s", "0", launcher=False, timeout=300)
+    assert line["n_gpus"] == world and len(line["per_gpu"]) == world
+    assert line["config"]["global_chunks"] == world * chunks
     assert line["parity_all_vs_golden"] is True and line["parity_first_4096_vs_golden"] is True
-    _check_identity(line, 2, chunks)
-    _check_rank_clocks(line, 2)
+    _check_identity(line, world, chunks)
+    if line["roofline"]["kernel"] == "k_sha1_fixed":
+        _check_rank_clocks(line, world)
+    else:  # the probe stamps the hot kernel only
+        assert line["clock"] is None and all(p["in_kernel_mhz"] is None for p in line["per_gpu"])
 
 
 @pytest.mark.parametrize("launcher", [True, False])

@@ -682,6 +682,10 @@ def main():
                          "GPU, recorded in the line); without it such a launch exits before the timed region")
     args = ap.parse_args()
 
+    if args.steps < 1 or args.warmup < 0 or args.chunks < 1:
+        print(f"bench.py: need --steps >= 1, --warmup >= 0 and --chunks >= 1 (got {args.steps}, {args.warmup}, "
+              f"{args.chunks})", file=sys.stderr, flush=True)
+        sys.exit(2)
     # Before torch is imported or any GPU call: --gpus decides the rank count.
     plan, err = rank_plan(args.gpus, os.environ)
     if err:

@@ -155,3 +155,18 @@ def test_ensure_built_adds_the_experiments_library_only_for_variants(monkeypatch
     assert calls == []
     b.ensure_built(experiments=True)
     assert len(calls) == 1 and calls[0][-1] == "experiments" and "lib" in calls[0]
+
+
+@pytest.mark.parametrize("bad", [["--steps", "0"], ["--warmup", "-1"], ["--chunks", "0"], ["--gpus", "0"]])
+def test_degenerate_arguments_exit_before_torch(bad):
+    """A line needs at least one timed step over at least one chunk on at
+    least one GPU: anything else exits 2 before torch is imported."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "-X", "importtime", BENCH, *bad], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 2 and not r.stdout.strip()
+    assert "bench.py:" in r.stderr
+    import re
+    assert not re.search(r"\|\s+torch\b", r.stderr)  # -X importtime lists every import: torch never was
+    assert re.search(r"\|\s+argparse\b", r.stderr)   # (and it does list them)

@@ -91,6 +91,10 @@ def _bench_worker(rank, world, port, q):
     h = StubHasher(py_oracle, lo, C)
     res = shard.run_rank(h, steps=4, warmup=2, world=world, rank=rank)
     assert h.steps == [-1, -2, 0, 1, 2, 3]
+    # the distinct-device exchange of the same launch: one GPU per rank on one node
+    ident = {"rank": rank, "host": "node0", "pci_bdf": f"0000:{0x05 + 0x10 * rank:02x}:00.0", "uuid": f"u{rank}"}
+    idents = shard.gather_objects(ident, world)
+    assert shard.check_distinct_devices(idents, world) is None and shard.distinct_devices(idents) == world
     if rank == 0:
         q.put((res["digests"], res["kernel_ms_max"], len(res["per_rank"])))
     else:
@@ -99,11 +103,13 @@ def _bench_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_bench_rank_protocol_two_ranks(oracle):
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_rank_protocol(oracle, world):
     """bench.py's own per-rank protocol (shard.run_rank: warmup, barriers,
-    timed steps, max over ranks, ordered digest gather) at world size 2 with a
-    CPU stub hasher: rank 0 ends up with all 12 digests in global order."""
-    world = 2
+    timed steps, max over ranks, ordered digest gather, and the pre-timing
+    identity exchange) with a CPU stub hasher, at world size 2 and at config
+    4's 8 ranks: rank 0 ends up with all 6 x world digests in global order and
+    the slowest rank's kernel time."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -114,9 +120,9 @@ def test_bench_rank_protocol_two_ranks(oracle):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    want = b"".join(oracle.hash_chunks(oracle.fill_synthetic(12 * CHUNK, 0, oracle.SEED_SYNTH), CHUNK))
+    want = b"".join(oracle.hash_chunks(oracle.fill_synthetic(6 * world * CHUNK, 0, oracle.SEED_SYNTH), CHUNK))
     assert dig == want
-    assert nranks == 2 and abs(kmax - 1.006) < 1e-9
+    assert nranks == world and abs(kmax - (1.0 + 6 * (world - 1) / 1000.0)) < 1e-9
 
 
 def _ident_worker(rank, world, port, shared, allow, q):

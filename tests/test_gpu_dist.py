@@ -52,6 +52,11 @@ def _run_bench(world, chunks, *extra, timeout=240, launcher=True, shared=True):
     --rehearse-shared-gpu (shared=True); without it bench.py must refuse."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
     env.pop("WORLD_SIZE", None)
+    if not shared:
+        # every rank on ONE device even on a box that shows several: the first
+        # of the devices this process may use
+        vis = env.get("HIP_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES")
+        env["HIP_VISIBLE_DEVICES"] = vis.split(",")[0] if vis else "0"
     args = [os.path.join(REPO, "bench.py"), "--gpus", str(world), "--chunks", str(chunks),
             "--steps", "3", "--warmup", "1", *extra] + (["--rehearse-shared-gpu"] if shared else [])
     if launcher:

@@ -47,11 +47,11 @@ tools: $(BIN)/make-chunks $(BIN)/verify-stream
 
 $(BIN)/make-chunks: $(PKG)/host/make_chunks_main.c $(LIB)
 	@mkdir -p $(BIN)
-	gcc -O2 -Wall -Wextra -Iinclude -o $@ $< -L$(PKG) -lbtsha1 -Wl,-rpath,'$$ORIGIN/..'
+	gcc -O2 -Wall -Wextra -Iinclude -pthread -o $@ $< -L$(PKG) -lbtsha1 -Wl,-rpath,'$$ORIGIN/..'
 
 $(BIN)/verify-stream: $(PKG)/host/verify_stream.c $(LIB)
 	@mkdir -p $(BIN)
-	gcc -O2 -Wall -Wextra -Iinclude -o $@ $< -L$(PKG) -lbtsha1 -Wl,-rpath,'$$ORIGIN/..'
+	gcc -O2 -Wall -Wextra -Iinclude -pthread -o $@ $< -L$(PKG) -lbtsha1 -Wl,-rpath,'$$ORIGIN/..'
 
 oracle:
 	$(MAKE) -C oracle
@@ -155,7 +155,7 @@ ubench: $(UB_BIN)
 tools/ubench/%: tools/ubench/%.hip $(CSRC)/sha1_device.h
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -I$(CSRC) -o $@ $<
 tools/ubench/residency: tools/ubench/residency.cpp $(LIB)
-	$(HIPCC) -O2 -std=c++17 -I$(CSRC) -o $@ $< -L$(PKG) -lbtsha1 -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
+	$(HIPCC) -O2 -std=c++17 -I$(CSRC) -pthread -o $@ $< -L$(PKG) -lbtsha1 -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
 
 # Install the drop-in for a reference build to link against:
 #   make install PREFIX=/opt/btsha1  ->  lib/libbtsha1.so, include/{sha.h,chunk.h,bt_sha1.h},
@@ -167,7 +167,7 @@ install: lib
 	install -m 644 include/sha.h include/chunk.h include/bt_sha1.h $(DESTDIR)$(PREFIX)/include/
 	gcc -O2 -Wall -Wextra -Iinclude -o $(DESTDIR)$(PREFIX)/bin/make-chunks $(PKG)/host/make_chunks_main.c \
 	    -L$(DESTDIR)$(PREFIX)/lib -lbtsha1 -Wl,-rpath,$(PREFIX)/lib
-	gcc -O2 -Wall -Wextra -Iinclude -o $(DESTDIR)$(PREFIX)/bin/verify-stream $(PKG)/host/verify_stream.c \
+	gcc -O2 -Wall -Wextra -Iinclude -o $(DESTDIR)$(PREFIX)/bin/verify-stream $(PKG)/host/verify_stream.c -pthread \
 	    -L$(DESTDIR)$(PREFIX)/lib -lbtsha1 -Wl,-rpath,$(PREFIX)/lib
 	printf 'prefix=%s\nlibdir=$${prefix}/lib\nincludedir=$${prefix}/include\n\nName: btsha1\nDescription: %s\nVersion: 3\nLibs: -L$${libdir} -lbtsha1 -Wl,-rpath,$${libdir}\nCflags: -I$${includedir}\n' \
 	    '$(PREFIX)' 'MI355X SHA-1 chunk hashing, drop-in for sha.h / chunk.h' > $(DESTDIR)$(PREFIX)/lib/pkgconfig/btsha1.pc

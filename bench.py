@@ -15,20 +15,24 @@ synchronize + barrier; value = all ranks' chunk bytes * K / max-over-ranks
 wall time, in GiB/s.  The hot kernel's own duration is also taken live with
 HIP events on the stream it is launched on, for the roofline.
 
-rank 0 at N=1 additionally reports, after the timed region:
-  * the in-kernel shader clock of the hot kernel (stamped diagnostic build,
-    bt_sha1_clock_probe), so the VALU roofline is priced at the clock the
-    chip actually held as well as at the nominal 2.4 GHz;
-  * cpu_baseline: the reference sha.c (oracle/_ref, compiled from the
+After the timed region:
+  * every rank: the in-kernel shader clock of the hot kernel (stamped
+    diagnostic build, bt_sha1_clock_probe), so the VALU roofline is priced
+    at the clock the chip actually held as well as at the nominal 2.4 GHz;
+  * every rank, all together: `power`, the socket power of its GPU from the
+    SMU energy accumulator while the timed step runs back to back for
+    --power-s seconds, against the board's power cap (the bound that sets
+    the hot kernel's clock, DESIGN.md §5);
+  * rank 0 at every N (the other ranks wait at the final barrier):
+    cpu_baseline, the reference sha.c (oracle/_ref, compiled from the
     reference) or our restatement (oracle/, "port") on the host cores, 4096
-    chunks of the same data at 1 thread and at every core this process may
-    use, at -O2 and at the reference Makefile's -O0 (SURVEY.md §8d);
-  * host_path: config 5, the PCIe-inclusive host->digest rates of the
-    pipelines that start in host memory (never `value`).
-Every rank (after the timed region, all together): `power`, the socket power
-of its GPU from the SMU energy accumulator while the timed step runs back to
-back for --power-s seconds, against the board's power cap (the bound that
-sets the hot kernel's clock).
+    of rank 0's chunks at 1 thread and at every core this process may use,
+    at -O2 and at the reference Makefile's -O0 (SURVEY.md §8d);
+  * rank 0 at N=1: verify_dev (the fused compare, paired with the hash) and
+    host_path, config 5's PCIe-inclusive host->digest rates of the pipelines
+    that start in host memory (never `value`): median of 5 steady runs with
+    each run's phase split, NUMA placement and cgroup throttling, and the
+    batched verifier fed zero-copy and packetized (util.c:275).
 """
 import argparse
 import ctypes
@@ -183,7 +187,14 @@ def relay(cmd, env=None):
         print(f"bench.py: the rank launch printed {len(lines)} result lines, expected exactly 1", file=sys.stderr,
               flush=True)
         return 1
-    return rc
+    return exit_status(rc)
+
+
+def exit_status(rc):
+    """A child's returncode as this process's exit status: a child killed by
+    signal S (returncode -S) becomes the shell's 128 + S, not sys.exit(-S)'s
+    256 - S, so the driver sees a signal death as one."""
+    return 128 - rc if rc < 0 else rc
 
 
 def spawn_ranks(n, argv):
@@ -322,37 +333,53 @@ class DeviceHasher:
 # Board power while the hot kernel runs (the kernel is bounded by
 # the board power limit, not by HBM or VALU issue)
 # ---------------------------------------------------------------------------
-def _smi_handle(torch, dev):
-    """(amdsmi module, processor handle of HIP device `dev` matched by PCI
-    address) -- a box may expose one GPU to HIP and several to amdsmi."""
+def _smi_matches(torch, dev):
+    """(amdsmi module, every processor handle at HIP device `dev`'s PCI
+    domain:bus:device) -- a box may expose one GPU to HIP and several to
+    amdsmi; partitions of one GPU share domain:bus:device and differ only in
+    the function number, which HIP does not report."""
     import amdsmi
     amdsmi.amdsmi_init()
     p = torch.cuda.get_device_properties(dev)
     want = (int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
+    hits = []
     for h in amdsmi.amdsmi_get_processor_handles():
         dom, bus, rest = amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")
         if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
-            return amdsmi, h
-    return amdsmi, None
+            hits.append(h)
+    return amdsmi, hits
+
+
+def _smi_handle(torch, dev):
+    """(amdsmi module, the first processor handle at HIP device `dev`'s PCI
+    address, or None) -- for the power reading (partitions share a socket)."""
+    smi, hits = _smi_matches(torch, dev)
+    return smi, (hits[0] if hits else None)
 
 
 def device_identity(torch, dev):
-    """Which physical GPU this rank drives: its host, its PCI address
-    (domain:bus:device.0, as HIP reports it) and the UUID amdsmi holds for
-    that address (the `uuid` HIP exposes through torch as a fallback), the HIP
-    device index, and how many devices the rank can see -- so an N > 1 line
-    proves it ran on N distinct GPUs (shard.check_distinct_devices; the host
-    keeps two nodes' equal PCI addresses apart)."""
+    """Which physical GPU this rank drives: its host; its PCI address as HIP
+    reports it (`pci_bdf`, domain:bus:device with the function number fixed
+    at .0 -- HIP does not expose it) and as amdsmi reports it (`smi_bdf`,
+    with the real function number); the UUID amdsmi holds for that address
+    (`uuid_source` "smi"), or the `uuid` HIP exposes through torch when
+    amdsmi fails ("hip", written differently for the same GPU); the HIP
+    device index and how many devices the rank can see -- so an N > 1 line
+    proves it ran on N distinct GPUs (shard.check_distinct_devices)."""
     p = torch.cuda.get_device_properties(dev)
     ident = {"pci_bdf": f"{int(p.pci_domain_id):04x}:{int(p.pci_bus_id):02x}:{int(p.pci_device_id):02x}.0",
-             "uuid": None, "hip_device": dev, "device_count": torch.cuda.device_count(), "name": p.name,
-             "host": socket.gethostname()}
+             "uuid": None, "uuid_source": None, "hip_device": dev, "device_count": torch.cuda.device_count(),
+             "name": p.name, "host": socket.gethostname()}
     smi = None
     try:
-        smi, h = _smi_handle(torch, dev)
-        if h is not None:
+        smi, hits = _smi_matches(torch, dev)
+        if len(hits) == 1:
+            h = hits[0]
             ident["uuid"] = str(smi.amdsmi_get_gpu_device_uuid(h))
+            ident["uuid_source"] = "smi"
             ident["smi_bdf"] = str(smi.amdsmi_get_gpu_device_bdf(h))
+        elif hits:  # which partition this HIP device is cannot be told apart: HIP's fields only
+            ident["smi_error"] = f"{len(hits)} amdsmi devices at this PCI address (partitions of one GPU)"
     except Exception as e:  # noqa: BLE001 -- identity falls back to HIP's own fields
         ident["smi_error"] = f"{type(e).__name__}: {e}"
     finally:
@@ -363,6 +390,7 @@ def device_identity(torch, dev):
                 pass
     if ident["uuid"] is None and getattr(p, "uuid", None) is not None:
         ident["uuid"] = str(p.uuid)
+        ident["uuid_source"] = "hip"
     return ident
 
 
@@ -557,49 +585,127 @@ def cpu_baseline(host_addr, n_chunks, gpu_digests, min_s=1.0, reps=3):
 # ---------------------------------------------------------------------------
 # Host paths (config 5): PCIe-inclusive, starting in host memory
 # ---------------------------------------------------------------------------
+def cgroup_cpu_stat():
+    """This process's cgroup CPU accounting (cgroup v2 cpu.stat): usage and
+    time throttled by the CPU quota, in seconds; None where unreadable."""
+    try:
+        d = dict(l.split() for l in open("/sys/fs/cgroup/cpu.stat") if l.strip())
+        return {"usage_s": int(d["usage_usec"]) / 1e6, "throttled_s": int(d.get("throttled_usec", 0)) / 1e6,
+                "nr_throttled": int(d.get("nr_throttled", 0))}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def timed_runs(fn, want, gib, steady=5, stats=None):
+    """The first run of a host path (it also pays one-time pinning), then
+    `steady` more; value = the MEDIAN steady run.  Every run is listed with
+    its wall time, the CPU time this process spent in it, the time the
+    cgroup's quota throttled it and -- with stats (bt.pipeline_stats) -- the
+    pipeline's own phase split: host staging (fill), blocked on the GPU lane
+    (wait), allocation (alloc)."""
+    import statistics
+    runs, ok = [], True
+    for _ in range(1 + steady):
+        cg0, cpu0 = cgroup_cpu_stat(), time.process_time()
+        t0 = time.perf_counter()
+        r = fn()
+        dt = time.perf_counter() - t0
+        cpu, cg1 = time.process_time() - cpu0, cgroup_cpu_stat()
+        ok = ok and r == want
+        row = {"GiB_per_s": round(gib / dt, 3), "s": round(dt, 4), "cpu_s": round(cpu, 3)}
+        if cg0 and cg1:
+            row["cgroup_throttled_s"] = round(cg1["throttled_s"] - cg0["throttled_s"], 4)
+        if stats is not None:
+            s = stats()
+            row.update(fill_s=s["fill_s"], wait_s=s["wait_s"], alloc_s=s["alloc_s"],
+                       fill_GiB_per_s=round(gib / s["fill_s"], 2) if s["fill_s"] > 0 else None)
+        runs.append(row)
+    steady_rates = [r["GiB_per_s"] for r in runs[1:]]
+    med = statistics.median(steady_rates)
+    out = {"GiB_per_s": round(med, 3), "first_run_GiB_per_s": runs[0]["GiB_per_s"],
+           "steady_min_max": [min(steady_rates), max(steady_rates)], "digests_match": ok,
+           "statistic": f"median of {steady} steady-state runs after the first", "runs": runs}
+    if stats is not None:
+        mid = sorted(runs[1:], key=lambda r: r["GiB_per_s"])[len(runs[1:]) // 2]
+        out["median_run_phases"] = {k: mid[k] for k in ("s", "fill_s", "wait_s", "alloc_s")}
+        out["median_run_phases"]["fill_frac"] = round(mid["fill_s"] / mid["s"], 3) if mid["s"] > 0 else None
+    return out
+
+
+def numa_view(st):
+    """NUMA placement of a pipeline run, from bt_sha1_get_pipeline_stats."""
+    return {"numa_nodes": st["numa_nodes"], "gpu_node": st["gpu_numa_node"], "policy": st["numa_policy"],
+            "image_pages_per_node": st["src_pages"], "lane_pages_per_node": st["lane_pages"],
+            "staging_pieces_per_cpu_node": st["copy_pieces"], "copy_threads": st["copy_threads"],
+            "method": "move_pages() over 64 sampled pages of the image / of each staging lane; staging pieces "
+                      "counted by the node of the CPU their thread started on; the GPU's node from "
+                      "/sys/bus/pci/devices/<bdf>/numa_node"}
+
+
+def run_verify_stream(vs, args, n, label, timeout=300):
+    """One bin/verify-stream run; its JSON summary beside the digests check."""
+    r = subprocess.run([vs, *args], capture_output=True, text=True, timeout=timeout)
+    lines = r.stdout.strip().splitlines()
+    try:
+        res = json.loads(lines[-1]) if lines else {}
+    except ValueError:
+        res = {}
+    row = {"GiB_per_s": res.get("GiB_per_s"),
+           "digests_match": r.returncode == 0 and res.get("failed") == 0 and res.get("ok") == res.get("chunks"),
+           "chunks_verified": res.get("chunks"), "timed_chunks": res.get("timed_chunks"),
+           "receive_threads": res.get("receive_threads"), "verifiers": res.get("verifiers"),
+           "path": f"bin/verify-stream {' '.join(args[:-2])}: {n} received chunks, {label}"}
+    if res.get("late_fills"):
+        row["late_fills"] = res["late_fills"]
+    if r.returncode != 0:
+        row["error"] = f"rc={r.returncode} {r.stderr[-300:]} {lines[-1:]}"
+    return row
+
+
 def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
     """host: pageable numpy image of the first chunks of dev_buf; want: their
-    device-resident digests.  Each rate is the best of 2 runs (the first run
-    of a path also pays its one-time pinned staging allocation)."""
+    device-resident digests.  Each pipeline rate is the median of 5
+    steady-state runs after a first run (which also pays the one-time pinned
+    staging allocation), every run listed with its phase split."""
     addr, nbytes = host.ctypes.data, host.nbytes
     gib = nbytes / 2**30
     out = {"image_GiB": round(gib, 3)}
 
-    def timed(fn, reps=2):
-        ts, ok = [], True
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            r = fn()
-            ts.append(time.perf_counter() - t0)
-            ok = ok and r == want
-        return round(gib / min(ts), 3), round(gib / ts[0], 3), ok
-
-    best, first, ok = timed(lambda: bt.chunks_host_addr(addr, nbytes))
-    out["pageable_chunks_host"] = {"GiB_per_s": best, "first_run_GiB_per_s": first, "digests_match": ok,
-                                   "path": "bt_sha1_chunks_host on pageable memory: threaded staging memcpy into "
-                                           "pinned lanes, 2-stream H2D, hot kernel, digests to pinned host"}
+    out["pageable_chunks_host"] = {
+        **timed_runs(lambda: bt.chunks_host_addr(addr, nbytes), want, gib, stats=bt.pipeline_stats),
+        "numa": numa_view(bt.pipeline_stats()),
+        "path": "bt_sha1_chunks_host on pageable memory: threaded staging memcpy into pinned lanes (on the "
+                "GPU's NUMA node), 2-stream H2D, hot kernel, digests to pinned host"}
     t0 = time.perf_counter()
     bt.host_register(addr, nbytes)
     reg_s = time.perf_counter() - t0
     try:
-        best, first, ok = timed(lambda: bt.chunks_host_addr(addr, nbytes))
-        out["registered_direct_dma"] = {"GiB_per_s": best, "first_run_GiB_per_s": first, "digests_match": ok,
-                                        "register_s": round(reg_s, 3),
-                                        "path": "bt_sha1_host_register'ed image, H2D straight from it, 2 streams"}
+        out["registered_direct_dma"] = {
+            **timed_runs(lambda: bt.chunks_host_addr(addr, nbytes), want, gib, stats=bt.pipeline_stats),
+            "register_s": round(reg_s, 3),
+            "path": "bt_sha1_host_register'ed image, H2D straight from it, 2 streams"}
         pin = torch.from_numpy(host)
         scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev_buf.device)
         rates = []
-        for _ in range(2):
+        for _ in range(3):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             scratch.copy_(pin, non_blocking=True)
             torch.cuda.synchronize()
-            rates.append(gib / (time.perf_counter() - t0))
-        out["raw_h2d_ceiling"] = {"GiB_per_s": round(max(rates), 3), "path": "one hipMemcpy of the registered image"}
+            rates.append(round(gib / (time.perf_counter() - t0), 3))
+        del scratch
+        out["raw_h2d_ceiling"] = {"GiB_per_s": max(rates), "runs": rates,
+                                  "path": "one hipMemcpy of the registered image (best of 3)"}
     finally:
         bt.host_unregister(addr)
-    # Zero-copy batched verifier (util.c:304-337 replacement): the product's C
-    # host tool, batch 1024 x 2 streams, over a 1 GiB image in a tmpfs file.
+    pg = out["pageable_chunks_host"]
+    pg["frac_of_raw_h2d"] = round(pg["GiB_per_s"] / out["raw_h2d_ceiling"]["GiB_per_s"], 4)
+    # The batched verifier (util.c:304-337 replacement): the product's C host
+    # tool over a 1 GiB image in a tmpfs file.  Zero-copy: the receive landed
+    # the bytes in the pinned slots once, the timed rounds re-verify them (the
+    # H2D + hash + verdict bound).  Packetized: every timed round receives
+    # each chunk again as util.c:275 does -- 1484-byte memcpys into the slot --
+    # on one receive thread, and on four (four verifiers, -g 4 -t).
     vs = os.path.join(PKG, "bin", "verify-stream")
     n = min(int(verify_gib * 2**30) // CHUNK, nbytes // CHUNK)
     import shutil
@@ -612,20 +718,17 @@ def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
         with open(lst, "w") as f:
             for i in range(n):
                 f.write(f"{i} {want[20 * i:20 * i + 20].hex()}\n")
-        rounds = 9
-        r = subprocess.run([vs, "-z", "-b", "1024", "-s", "2", "-r", str(rounds), img, lst],
-                           capture_output=True, text=True, timeout=300)
-        lines = r.stdout.strip().splitlines()
-        try:
-            res = json.loads(lines[-1]) if lines else {}
-        except ValueError:
-            res = {}
-        out["zero_copy_verifier"] = {
-            "GiB_per_s": res.get("GiB_per_s"), "digests_match": r.returncode == 0 and res.get("failed") == 0
-            and res.get("ok") == res.get("chunks"), "chunks_verified": res.get("chunks"),
-            "path": f"bin/verify-stream -z -b 1024 -s 2: {n} received chunks in pinned verifier slots, "
-                    f"{rounds - 1} steady-state rounds timed (H2D + hash + fused memcmp + verdicts)",
-            **({} if r.returncode == 0 else {"error": f"rc={r.returncode} {r.stderr[-300:]} {lines[-1:]}"})}
+        out["zero_copy_verifier"] = run_verify_stream(
+            vs, ["-z", "-b", "1024", "-s", "2", "-r", "9", img, lst], n,
+            "in pinned verifier slots, 8 steady-state rounds timed (H2D + hash + fused memcmp + verdicts)")
+        out["packetized_verifier"] = run_verify_stream(
+            vs, ["-b", "1024", "-s", "2", "-r", "3", "-w", "1", img, lst], n,
+            "each received again in every timed round as util.c:275 does (1484-byte memcpys into a pinned "
+            "slot), one receive thread, 2 rounds timed after 1 untimed")
+        out["packetized_verifier_4_threads"] = run_verify_stream(
+            vs, ["-g", "4", "-t", "-b", "256", "-s", "2", "-r", "3", "-w", "1", img, lst], n,
+            "1484-byte memcpys as util.c:275, chunk id mod 4 -> 4 verifiers on this GPU, one receive thread "
+            "each, 2 rounds timed after 1 untimed")
     return out
 
 
@@ -841,11 +944,16 @@ def main():
         traffic, traffic_note = find_traffic(want, args.traffic_json)
         phase("gather_and_parity_s")
 
+        # Rank 0 runs the CPU baseline at every N (the other ranks wait at the
+        # final barrier, their GPUs idle): each line carries the reference
+        # sha.c on this node's host cores from the same run (north_star).
+        # The host paths (config 5) are a one-GPU measurement (N = 1 only).
+        want_host = world == 1 and not args.no_host_path
         extras_host = None
-        if world == 1 and (not args.no_cpu_baseline or not args.no_host_path):
+        if not args.no_cpu_baseline or want_host:
             import numpy as np
             n_host = min(C, max(args.cpu_chunks if not args.no_cpu_baseline else 0,
-                                0 if args.no_host_path else int(args.host_gib * 2**30) // CHUNK))
+                                int(args.host_gib * 2**30) // CHUNK if want_host else 0))
             extras_host = np.empty(n_host * CHUNK, dtype=np.uint8)
             view = torch.from_numpy(extras_host)
             for i in range(0, n_host, 2048):  # 1 GiB slices
@@ -857,7 +965,7 @@ def main():
                         view[j * CHUNK:(j + 1) * CHUNK].copy_(hasher.buf[j * pitch:j * pitch + CHUNK])
 
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:
             try:
                 cpu = cpu_baseline(extras_host.ctypes.data, min(args.cpu_chunks, C), all_dig)
             except Exception as e:  # the checker must never cost the bench line
@@ -873,7 +981,7 @@ def main():
             phase("verify_dev_s")
 
         host = None
-        if world == 1 and not args.no_host_path and pitch == CHUNK:
+        if want_host and pitch == CHUNK:
             try:
                 n_img = min(C, int(args.host_gib * 2**30) // CHUNK)
                 host = host_paths(bt, torch, hasher.buf, extras_host[:n_img * CHUNK], all_dig[:20 * n_img])

@@ -40,6 +40,20 @@ class SHA1Context(ctypes.Structure):  # include/sha.h (reference sha.h:39-50 lay
                 ("bufferLength", ctypes.c_uint32), ("buffer", ctypes.c_uint8 * 64)]
 
 
+STATS_NODES = 8  # BT_SHA1_STATS_NODES
+
+
+class PipelineStats(ctypes.Structure):  # include/bt_sha1.h bt_sha1_pipeline_stats
+    _fields_ = [("chunks", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64),
+                ("batches", ctypes.c_uint32), ("staged", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("copy_threads", ctypes.c_int32), ("numa_nodes", ctypes.c_int32),
+                ("gpu_numa_node", ctypes.c_int32), ("numa_policy", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("total_s", ctypes.c_double), ("alloc_s", ctypes.c_double), ("fill_s", ctypes.c_double),
+                ("wait_s", ctypes.c_double),
+                ("lane_pages", ctypes.c_int32 * STATS_NODES), ("src_pages", ctypes.c_int32 * STATS_NODES),
+                ("copy_pieces", ctypes.c_int32 * STATS_NODES)]
+
+
 def _sig(name, res, *args):
     f = getattr(lib, name)
     f.restype = res
@@ -71,6 +85,7 @@ _sig("bt_sha1_wallclock_khz", _i64)
 _sig("bt_sha1_debug_barrier_stats", ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int)
 _sig("bt_sha1_debug_dropin_residue", _i64, ctypes.c_int)
 _sig("bt_sha1_chunks_file", _i64, _vp, _u64, _vp, _u64)
+_sig("bt_sha1_get_pipeline_stats", ctypes.c_int, ctypes.POINTER(PipelineStats))
 _sig("bt_sha1_verifier_create", _vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32)
 _sig("bt_sha1_verifier_destroy", None, _vp)
 _sig("bt_sha1_verifier_slot", _vp, _vp)
@@ -298,6 +313,22 @@ def chunks_host_addr(addr, nbytes, chunk_len=CHUNK, ndev=None, devs=None):
     out = (ctypes.c_uint8 * max(20 * nch, 1))()
     got = _host_split(addr, nbytes, chunk_len, out, ndev, devs)
     return bytes(out)[:20 * got]
+
+
+def pipeline_stats():
+    """Phase times and NUMA placement of this thread's last host pipeline run
+    (bt_sha1_get_pipeline_stats) as a dict; per-node tallies are trimmed to
+    the machine's node count."""
+    s = PipelineStats()
+    _check(lib.bt_sha1_get_pipeline_stats(ctypes.byref(s)), "bt_sha1_get_pipeline_stats")
+    nodes = max(1, min(STATS_NODES, s.numa_nodes))
+    d = {k: getattr(s, k) for k, _ in PipelineStats._fields_ if k != "reserved"}
+    for k in ("lane_pages", "src_pages", "copy_pieces"):
+        d[k] = list(d[k])[:nodes]
+    for k in ("total_s", "alloc_s", "fill_s", "wait_s"):
+        d[k] = round(d[k], 4)
+    d["staged"], d["numa_policy"] = bool(s.staged), ("gpu" if s.numa_policy else "none")
+    return d
 
 
 def shahash(data):

@@ -27,8 +27,11 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 #include <cerrno>
 
@@ -126,6 +129,154 @@ struct PinBuf {
   T *as() const { return static_cast<T *>(p); }
 };
 
+// ---- NUMA placement of the host pipelines' staging ---------------------------
+// The GPU hangs off one socket's PCIe root.  The staging lanes are written by
+// the copy threads and read by the DMA engine; placing their pages on the
+// GPU's node and running the copy threads on that node's CPUs keeps both
+// local (the caller's pageable input is wherever the caller touched it).
+// Topology from sysfs, no libnuma: node N's CPUs from
+// /sys/devices/system/node/nodeN/cpulist, the GPU's node from
+// /sys/bus/pci/devices/<bdf>/numa_node.
+struct NumaTopo {
+  int nodes = 1;
+  std::vector<int> cpu_node;               // cpu -> node
+  std::vector<std::vector<int>> node_cpus;  // node -> cpus
+};
+
+std::vector<int> parse_cpulist(const char *s) {
+  std::vector<int> out;
+  while (*s) {
+    char *end = nullptr;
+    const long a = strtol(s, &end, 10);
+    if (end == s) break;
+    long b = a;
+    s = end;
+    if (*s == '-') {
+      b = strtol(s + 1, &end, 10);
+      s = end;
+    }
+    for (long c = a; c <= b && c < 65536; ++c) out.push_back((int)c);
+    while (*s == ',' || *s == '\n' || *s == ' ') ++s;
+  }
+  return out;
+}
+
+const NumaTopo &numa_topo() {
+  static const NumaTopo t = [] {
+    NumaTopo r;
+    int present = 0;
+    for (int n = 0; n < 256; ++n) {
+      char path[96], buf[4096];
+      snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", n);
+      FILE *f = fopen(path, "r");
+      if (!f) continue;
+      const size_t got = fread(buf, 1, sizeof buf - 1, f);
+      fclose(f);
+      buf[got] = 0;
+      ++present;
+      r.node_cpus.resize(n + 1);
+      r.node_cpus[n] = parse_cpulist(buf);
+      for (int c : r.node_cpus[n]) {
+        if ((int)r.cpu_node.size() <= c) r.cpu_node.resize(c + 1, -1);
+        r.cpu_node[c] = n;
+      }
+    }
+    r.nodes = std::max(1, present);
+    return r;
+  }();
+  return t;
+}
+
+int node_of_cpu(int cpu) {
+  const NumaTopo &t = numa_topo();
+  return cpu >= 0 && cpu < (int)t.cpu_node.size() ? t.cpu_node[cpu] : -1;
+}
+
+// The NUMA node the device's PCI function reports (-1: unknown).
+int gpu_numa_node(int dev) {
+  char bdf[64] = {0};
+  if (hipDeviceGetPCIBusId(bdf, sizeof bdf, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  for (char *p = bdf; *p; ++p)
+    if (*p >= 'A' && *p <= 'F') *p = (char)(*p + 32);
+  char path[160];
+  snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bdf);
+  FILE *f = fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (fscanf(f, "%d", &node) != 1) node = -1;
+  fclose(f);
+  return node;
+}
+
+// BT_SHA1_NUMA=off disables the placement; default (or "gpu"): place when the
+// machine has more than one node and the GPU's node is known.
+bool numa_placement_wanted() {
+  static const bool on = [] {
+    const char *e = getenv("BT_SHA1_NUMA");
+    return !(e && (!strcmp(e, "off") || !strcmp(e, "0")));
+  }();
+  return on;
+}
+
+// Pages of [p, p+len) sampled evenly (at most `samples`), counted per node
+// (move_pages with no target nodes only queries).  Pages not yet faulted in
+// count nowhere.
+void page_nodes(const void *p, uint64_t len, int samples, int32_t *counts, int ncounts) {
+  if (!p || !len || samples <= 0) return;
+  const uint64_t pg = 4096, first = (uintptr_t)p & ~(pg - 1), last = ((uintptr_t)p + len - 1) & ~(pg - 1);
+  const uint64_t npages = (last - first) / pg + 1;
+  const int n = (int)std::min<uint64_t>((uint64_t)samples, npages);
+  std::vector<void *> pages(n);
+  std::vector<int> status(n, -1);
+  for (int i = 0; i < n; ++i) pages[i] = (void *)(first + pg * (npages * (uint64_t)i / (uint64_t)n));
+  if (syscall(SYS_move_pages, 0, (unsigned long)n, pages.data(), nullptr, status.data(), 0) != 0) return;
+  for (int s : status)
+    if (s >= 0 && s < ncounts) ++counts[s];
+}
+
+// Staging placement of one call: the node to bind the lanes to and the CPUs
+// (within the calling thread's affinity mask) the copy threads run on.
+struct Placement {
+  int node = -1;      // -1: no placement
+  int ncpus = 0;      // 0: threads unpinned
+  cpu_set_t cpus;
+};
+
+Placement placement_for(int gpu_node) {
+  Placement pl;
+  CPU_ZERO(&pl.cpus);
+  const NumaTopo &t = numa_topo();
+  if (!numa_placement_wanted() || gpu_node < 0 || t.nodes < 2 || gpu_node >= (int)t.node_cpus.size()) return pl;
+  cpu_set_t aff;
+  CPU_ZERO(&aff);
+  if (sched_getaffinity(0, sizeof aff, &aff) != 0) return pl;
+  for (int c : t.node_cpus[gpu_node])
+    if (c < CPU_SETSIZE && CPU_ISSET(c, &aff)) {
+      CPU_SET(c, &pl.cpus);
+      ++pl.ncpus;
+    }
+  if (pl.ncpus == 0) return pl;  // none of the GPU's CPUs usable: leave placement to the kernel
+  pl.node = gpu_node;
+  return pl;
+}
+
+// Preferred (not strict) policy: pages go to `node` while it has memory.
+void prefer_node(void *p, size_t len, int node) {
+  if (node < 0 || node >= 256) return;
+  unsigned long mask[4] = {0, 0, 0, 0};
+  mask[node / 64] = 1ul << (node % 64);
+  const int kMpolPreferred = 1;
+  (void)syscall(SYS_mbind, p, (unsigned long)len, kMpolPreferred, mask, 256ul, 0u);
+}
+
+// The calling thread's current placement (set by run_pipeline for the
+// duration of one call; read by the staging helpers on that thread).
+thread_local const Placement *t_place = nullptr;
+thread_local std::atomic<int32_t> *t_piece_nodes = nullptr;  // per-node piece tally of the call
+
 void touch_parallel(uint8_t *p, uint64_t n);
 
 // Grow-only staging buffer of the host pipelines, read only by the DMA engine
@@ -144,7 +295,8 @@ struct StageBuf {
     p = nullptr;
     cap = 0;
   }
-  int ensure(size_t need) {
+  // node >= 0: the pages prefer that NUMA node (placed at first touch).
+  int ensure(size_t need, int node = -1) {
     if (need <= cap) return 0;
     release();
     const size_t sz = (std::max<size_t>(need, 4096) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
@@ -157,6 +309,7 @@ struct StageBuf {
     // Not inherited by fork(): a child (e.g. a subprocess about to exec) would
     // otherwise get a copy of every page-locked page at fork time.
     (void)madvise(q, sz, MADV_DONTFORK);
+    prefer_node(q, sz, node);
     touch_parallel((uint8_t *)q, sz);
     const hipError_t e = hipHostRegister(q, sz, hipHostRegisterPortable);
     if (e != hipSuccess) {
@@ -186,6 +339,7 @@ struct Lane {
 
 struct DevCtx {
   int dev = 0;
+  int numa_node = -2;  // the GPU's NUMA node (-1 unknown; -2 not read yet)
   std::mutex mu;
   hipStream_t s = nullptr;  // drop-in calls and NULL-stream launches (= lane[0].s)
   Lane lane[2];
@@ -374,17 +528,31 @@ int copy_threads() {
 
 // Split [0, n) into page-aligned pieces of at least 16 MiB, one per thread
 // (the caller's thread takes the first), and run body(off, len, piece) on each.
+// Under a pipeline call's NUMA placement (t_place) every piece runs on a
+// helper thread pinned to the GPU node's CPUs (the caller's own affinity is
+// left alone); staging pieces (tally) are counted by the node of the CPU
+// they started on.
 template <class Body>
-void parallel_pieces(uint64_t n, Body body) {
+void parallel_pieces(uint64_t n, Body body, bool tally = false) {
   const uint64_t min_piece = 16ull << 20;
   int t = copy_threads();
   if ((uint64_t)t > n / min_piece) t = (int)std::max<uint64_t>(1, n / min_piece);
   uint64_t piece = (n + t - 1) / t;
   piece = (piece + 4095) & ~4095ull;
+  const Placement *pl = t_place;
+  std::atomic<int32_t> *counts = tally ? t_piece_nodes : nullptr;
+  const bool pin = pl && pl->ncpus > 0;
+  auto run = [&, pl, counts, pin](int i) {
+    if (pin) (void)pthread_setaffinity_np(pthread_self(), sizeof pl->cpus, &pl->cpus);
+    if (counts) {
+      const int nd = node_of_cpu(sched_getcpu());
+      if (nd >= 0 && nd < BT_SHA1_STATS_NODES) counts[nd].fetch_add(1, std::memory_order_relaxed);
+    }
+    body((uint64_t)i * piece, std::min<uint64_t>(piece, n - (uint64_t)i * piece), i);
+  };
   std::vector<std::thread> th;
-  for (int i = 1; i < t && (uint64_t)i * piece < n; ++i)
-    th.emplace_back([&, i] { body((uint64_t)i * piece, std::min<uint64_t>(piece, n - (uint64_t)i * piece), i); });
-  body(0, std::min<uint64_t>(piece, n), 0);
+  for (int i = pin ? 0 : 1; i < t && (uint64_t)i * piece < n; ++i) th.emplace_back(run, i);
+  if (!pin) run(0);
   for (auto &x : th) x.join();
 }
 
@@ -395,11 +563,15 @@ void touch_parallel(uint8_t *p, uint64_t n) {
 }
 
 void parallel_copy(uint8_t *dst, const uint8_t *src, uint64_t n) {
-  if (n < (32ull << 20)) {
+  if (n < (32ull << 20) && !(t_place && t_place->ncpus > 0)) {
+    if (t_piece_nodes) {
+      const int nd = node_of_cpu(sched_getcpu());
+      if (nd >= 0 && nd < BT_SHA1_STATS_NODES) t_piece_nodes[nd].fetch_add(1, std::memory_order_relaxed);
+    }
     memcpy(dst, src, n);
     return;
   }
-  parallel_pieces(n, [&](uint64_t off, uint64_t len, int) { memcpy(dst + off, src + off, len); });
+  parallel_pieces(n, [&](uint64_t off, uint64_t len, int) { memcpy(dst + off, src + off, len); }, true);
 }
 
 // pread `want` bytes at file offset `pos` into dst with several threads.
@@ -422,7 +594,7 @@ int64_t parallel_pread(int fd, uint8_t *dst, uint64_t want, uint64_t pos) {
       done += (uint64_t)r;
     }
     got[i] = (int64_t)done;
-  });
+  }, true);
   if (err) return -1;
   int64_t total = 0;
   for (int i = 0; i < 64 && asked[i]; ++i) {
@@ -472,6 +644,10 @@ bool serial_copies(bool staged) {
   return forced >= 0 ? forced == 1 : !staged;
 }
 
+// bt_sha1_get_pipeline_stats: the calling thread's last pipeline run.
+thread_local bt_sha1_pipeline_stats t_stats;
+thread_local bool t_stats_valid = false;
+
 template <class Fill, class Sink>
 int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool staged, Fill fill, Sink sink) {
   if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
@@ -484,11 +660,30 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   const uint64_t bytes_per = batch_bytes_for(chunk_len, size_hint, staged);
   const uint64_t per = bytes_per / chunk_len;
   double t_alloc = 0;
+  // NUMA: staged lanes on the GPU's node, staging threads on its CPUs.
+  if (c->numa_node == -2) c->numa_node = gpu_numa_node(c->dev);
+  const Placement place = staged ? placement_for(c->numa_node) : Placement{};
+  std::atomic<int32_t> piece_nodes[BT_SHA1_STATS_NODES];
+  for (auto &x : piece_nodes) x.store(0);
+  struct PlaceScope {  // the staging helpers of this thread see the placement for this call only
+    const Placement *prev_place;
+    std::atomic<int32_t> *prev_nodes;
+    PlaceScope(const Placement *p, std::atomic<int32_t> *n) : prev_place(t_place), prev_nodes(t_piece_nodes) {
+      t_place = p;
+      t_piece_nodes = n;
+    }
+    ~PlaceScope() {
+      t_place = prev_place;
+      t_piece_nodes = prev_nodes;
+    }
+  } place_scope(&place, piece_nodes);
+  t_stats_valid = false;
   // Buffers are sized (grow-only, kept across calls) when a lane is first
   // used: an input that fits one batch never pins the second lane's memory.
   auto prepare = [&](Lane &l) -> int {
     const double t0 = now_s();
-    if ((staged && l.h_in.ensure(bytes_per)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per)) return -1;
+    if ((staged && l.h_in.ensure(bytes_per, place.node)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per))
+      return -1;
     t_alloc += now_s() - t0;
     return 0;
   };
@@ -507,7 +702,9 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
         return;
       }
       Lane &l = c->lane[1];
-      pre_rc = (staged && l.h_in.ensure(bytes_per)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per) ? -1 : 0;
+      pre_rc = (staged && l.h_in.ensure(bytes_per, place.node)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per)
+                   ? -1
+                   : 0;
       if (pre_rc) pre_err = t_err;
     });
   }
@@ -585,14 +782,41 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
       DevBuf &d = c->lane[i].d_in;
       if (d.cap <= keep) continue;
       d.release();
-      if (kept_cap[i] && d.ensure(std::min<uint64_t>(kept_cap[i], keep))) return -1;
+      // Every digest has gone through the sink: the kept lane is only a
+      // cache, so a failed re-allocation leaves it released (the next
+      // call's prepare() grows it again) and the call still succeeds.
+      if (kept_cap[i] && d.ensure(std::min<uint64_t>(kept_cap[i], keep))) {
+        (void)hipGetLastError();
+        t_err.clear();
+      }
     }
   }
+  const double total = now_s() - t_start;
+  bt_sha1_pipeline_stats &s = t_stats;
+  memset(&s, 0, sizeof s);
+  s.chunks = next;
+  s.bytes = 0;
+  s.batch_bytes = bytes_per;
+  s.batches = (uint32_t)k;
+  s.staged = staged ? 1 : 0;
+  s.device = c->dev;
+  s.copy_threads = copy_threads();
+  s.numa_nodes = numa_topo().nodes;
+  s.gpu_numa_node = c->numa_node;
+  s.numa_policy = place.node >= 0 ? 1 : 0;
+  s.total_s = total;
+  s.alloc_s = t_alloc;
+  s.fill_s = t_fill;
+  s.wait_s = t_wait;
+  if (staged)
+    for (auto &l : c->lane) page_nodes(l.h_in.p, l.h_in.cap, 64, s.lane_pages, BT_SHA1_STATS_NODES);
+  for (int i = 0; i < BT_SHA1_STATS_NODES; ++i) s.copy_pieces[i] = piece_nodes[i].load();
+  t_stats_valid = true;
   if (trace_on())
     fprintf(stderr, "libbtsha1 pipeline dev %d: %llu chunks, batch %llu B, %s: total %.4f s = alloc %.4f + fill %.4f "
                     "+ wait %.4f + other\n",
             c->dev, (unsigned long long)next, (unsigned long long)bytes_per, staged ? "staged" : "direct DMA",
-            now_s() - t_start, t_alloc, t_fill, t_wait);
+            total, t_alloc, t_fill, t_wait);
   return (int64_t)next;
 }
 
@@ -623,7 +847,12 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   };
 
   auto sink = [&](uint64_t first, uint64_t count, const uint8_t *d) { memcpy(h_dig + 20 * first, d, 20 * count); };
-  return run_pipeline(c, chunk_len, total, !pinned, fill, sink);
+  const int64_t n = run_pipeline(c, chunk_len, total, !pinned, fill, sink);
+  if (n >= 0 && t_stats_valid) {
+    t_stats.bytes = total;
+    page_nodes(h_in, total, 64, t_stats.src_pages, BT_SHA1_STATS_NODES);
+  }
+  return n;
 }
 
 template <class Sink>
@@ -669,7 +898,14 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
     }
     return (int64_t)got;
   };
-  const int64_t n = run_pipeline(c, chunk_len, hint, true, fill, sink);
+  uint64_t bytes_in = 0;
+  auto counted_fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src) -> int64_t {
+    const int64_t r = fill(l, at, max, src);
+    if (r > 0) bytes_in += (uint64_t)r;
+    return r;
+  };
+  const int64_t n = run_pipeline(c, chunk_len, hint, true, counted_fill, sink);
+  if (n >= 0 && t_stats_valid) t_stats.bytes = bytes_in;
   if (regular) {
     // Leave the stream where the reference's fread loop leaves it: at EOF,
     // with the end-of-file indicator set.
@@ -1140,6 +1376,19 @@ int64_t bt_sha1_chunks_host_multi(const void *h_in, uint64_t total_len, uint64_t
   return bt_sha1_chunks_host_devices(h_in, total_len, chunk_len, h_digests, devs.data(), ndev);
 }
 
+int bt_sha1_get_pipeline_stats(bt_sha1_pipeline_stats *out) {
+  if (!out) {
+    set_err("null pointer");
+    return -1;
+  }
+  if (!t_stats_valid) {
+    set_err("no host pipeline has run on this thread");
+    return -1;
+  }
+  *out = t_stats;
+  return 0;
+}
+
 int64_t bt_sha1_chunks_file(void *fp, uint64_t chunk_len, uint8_t *h_digests, uint64_t max_chunks) {
   if (!fp || !h_digests) {
     set_err("null pointer");
@@ -1408,11 +1657,20 @@ bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32
     set_err("verifier: chunk_len must be a 16-byte multiple <= 32 MiB and batch > 0");
     return nullptr;
   }
-  if (!ctx_for(device)) return nullptr;
+  DevCtx *c = ctx_for(device);
+  if (!c) return nullptr;
   KeepDevice keep_dev;
   if (hipSetDevice(device) != hipSuccess) {
     set_err("hipSetDevice(%d) failed", device);
     return nullptr;
+  }
+  // The receive slots are written by the caller's receive path and read by
+  // the DMA engine: on the GPU's NUMA node, like the pipelines' lanes.
+  int node = -1;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->numa_node == -2) c->numa_node = gpu_numa_node(device);
+    node = placement_for(c->numa_node).node;
   }
   auto *v = new bt_sha1_verifier;
   v->dev = device;
@@ -1426,7 +1684,7 @@ bt_sha1_verifier *bt_sha1_verifier_create(int device, uint32_t chunk_len, uint32
     b.state.assign(batch, 0);
     if (hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess ||
-        b.slots.ensure(bytes) != 0 ||
+        b.slots.ensure(bytes, node) != 0 ||
         hipHostMalloc((void **)&b.h_exp, 20 * (size_t)batch, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&b.h_ok, batch, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&b.h_dig, 20 * (size_t)batch, hipHostMallocDefault) != hipSuccess ||

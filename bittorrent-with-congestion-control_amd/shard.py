@@ -67,16 +67,45 @@ def gather_objects(obj, world, group=None):
     return out
 
 
-def device_key(ident):
-    """One physical GPU: (host, PCI address, UUID).  The host keeps two nodes'
-    equal PCI addresses apart (a multi-node launch); the UUID can only split
-    keys further (never merge two GPUs), e.g. partitions behind one address."""
-    return (ident.get("host"), ident.get("pci_bdf"), ident.get("uuid"))
+def _bdf(addr, with_function=True):
+    """A PCI address in one spelling: lowercase, 4-digit domain; without the
+    function number when with_function is False."""
+    if not addr:
+        return None
+    a = str(addr).strip().lower()
+    if a.count(":") == 1:  # bus:device.function without a domain
+        a = "0000:" + a
+    dom, bus, rest = a.split(":", 2)
+    dev, _, fn = rest.partition(".")
+    out = f"{int(dom, 16):04x}:{int(bus, 16):02x}:{int(dev, 16):02x}"
+    return f"{out}.{int(fn or '0', 16)}" if with_function else out
+
+
+def device_keys(idents):
+    """One key per rank naming the physical GPU it drove: (host, PCI address,
+    UUID), every rank's key built the same way, so one GPU can never get two
+    keys because two ranks read it through different sources:
+      * the address is amdsmi's full domain:bus:device.function (`smi_bdf`)
+        when EVERY rank has it -- partitions of one GPU differ only in the
+        function number -- else HIP's domain:bus:device for every rank
+        (`pci_bdf` without its fixed .0: the coarser key, so two partitions
+        then count as one GPU rather than one GPU as two);
+      * the UUID only when every rank got it from the same source (amdsmi
+        and HIP spell one GPU's UUID differently), else none;
+      * the host keeps two nodes' equal PCI addresses apart (multi-node)."""
+    full = bool(idents) and all(i.get("smi_bdf") for i in idents)
+    sources = {i.get("uuid_source") for i in idents}
+    same_uuid = len(sources) == 1 and None not in sources
+    keys = []
+    for i in idents:
+        addr = _bdf(i.get("smi_bdf")) if full else _bdf(i.get("pci_bdf"), with_function=False)
+        keys.append((i.get("host"), addr, i.get("uuid") if same_uuid else None))
+    return keys
 
 
 def distinct_devices(idents):
     """How many distinct GPUs the ranks drove (bench.py's `distinct_gpus`)."""
-    return len({device_key(i) for i in idents})
+    return len(set(device_keys(idents)))
 
 
 def check_distinct_devices(idents, world, allow_shared=False):
@@ -95,8 +124,8 @@ def check_distinct_devices(idents, world, allow_shared=False):
     if allow_shared:
         return None
     seen = {}
-    for i in idents:
-        seen.setdefault(device_key(i), []).append(i.get("rank"))
+    for i, key in zip(idents, device_keys(idents)):
+        seen.setdefault(key, []).append(i.get("rank"))
     if len(seen) == world:
         return None
     dup = {k: ranks for k, ranks in seen.items() if len(ranks) > 1}

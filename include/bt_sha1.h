@@ -173,6 +173,46 @@ int64_t bt_sha1_chunks_host_devices(const void *h_in, uint64_t total_len, uint64
 int64_t bt_sha1_chunks_file(void *fp /* FILE* */, uint64_t chunk_len, uint8_t *h_digests,
                             uint64_t max_chunks);
 
+/* Where the time of the calling thread's last host pipeline run went
+ * (bt_sha1_chunks_host, bt_sha1_chunks_file, make_chunks; for the multi-GPU
+ * split, the last worker's run on its own thread), and where its memory sat.
+ * The pipeline stages each batch on the host (fill: threaded memcpy / pread
+ * into the page-locked staging lanes, or nothing for DMA straight from
+ * pinned input), queues its H2D and hash on the lane's stream, and blocks
+ * (wait) only when a lane is needed again or at the end.  fill_s close to
+ * total_s means the host staging sets the rate; wait_s close to total_s
+ * means PCIe / the GPU do.  NUMA fields (Linux sysfs + move_pages): the
+ * GPU's node, sampled pages of the staging lanes and of the caller's input
+ * per node, and the staging pieces by the node of the CPU their thread ran
+ * on; -1 / zeros where unknown.  numa_policy: 1 when the lanes were placed
+ * on the GPU's node and the staging threads ran on that node's CPUs within
+ * the caller's affinity mask (BT_SHA1_NUMA=gpu, the default when the GPU's
+ * node is known and the machine has more than one node), 0 when not
+ * (BT_SHA1_NUMA=off, one node, or no usable CPU of the GPU's node).
+ * Returns 0, or -1 when this thread has run no pipeline. */
+#define BT_SHA1_STATS_NODES 8
+typedef struct {
+  uint64_t chunks;          /* digests produced                               */
+  uint64_t bytes;           /* input bytes                                    */
+  uint64_t batch_bytes;     /* bytes per lane batch                           */
+  uint32_t batches;         /* lane batches launched                          */
+  int32_t staged;           /* 1: copied into the lanes; 0: direct DMA        */
+  int32_t device;           /* HIP device                                     */
+  int32_t copy_threads;     /* staging threads per piece (BT_SHA1_COPY_THREADS) */
+  int32_t numa_nodes;       /* NUMA nodes of the machine (sysfs)              */
+  int32_t gpu_numa_node;    /* the GPU's node (-1: unknown)                   */
+  int32_t numa_policy;      /* see above                                      */
+  int32_t reserved;
+  double total_s;           /* the whole call                                 */
+  double alloc_s;           /* lane allocation / page-locking in the call     */
+  double fill_s;            /* host staging (memcpy / pread) on the host      */
+  double wait_s;            /* blocked on a lane's H2D + hash                 */
+  int32_t lane_pages[BT_SHA1_STATS_NODES];  /* sampled staging pages per node */
+  int32_t src_pages[BT_SHA1_STATS_NODES];   /* sampled input pages per node   */
+  int32_t copy_pieces[BT_SHA1_STATS_NODES]; /* staging pieces per CPU node    */
+} bt_sha1_pipeline_stats;
+int bt_sha1_get_pipeline_stats(bt_sha1_pipeline_stats *out);
+
 /* ---- batched asynchronous verify (replaces util.c:304-337's hash+memcmp) -- */
 typedef struct bt_sha1_verifier bt_sha1_verifier;
 typedef struct {

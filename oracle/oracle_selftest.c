@@ -128,9 +128,14 @@ int main(void) {
     _exit(rh == -1 && rs == -1 ? 0 : 5);
   }
   int st = 0;
-  if (pid > 0 && waitpid(pid, &st, 0) == pid && WIFEXITED(st) && WEXITSTATUS(st) == 7) {
+  /* a failed fork or waitpid is a failure, never a pass on the zeroed status */
+  const pid_t w = pid > 0 ? waitpid(pid, &st, 0) : -1;
+  if (w != pid) {
+    printf("FAIL thread-creation check: fork/waitpid failed (pid %d, waitpid %d)\n", (int)pid, (int)w);
+    fails++;
+  } else if (WIFEXITED(st) && WEXITSTATUS(st) == 7) {
     puts("skip thread-creation check: cannot drop to an unprivileged user here");
-  } else if (pid < 0 || !WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+  } else if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
     printf("FAIL thread-creation failure not reported cleanly (status %d)\n", st);
     fails++;
   }

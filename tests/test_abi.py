@@ -101,6 +101,39 @@ def test_dropin_residue_hook_needs_no_device():
         bt.debug_dropin_residue(-1)
 
 
+def test_pipeline_stats_layout_and_no_run_error(tmp_path):
+    """bt_sha1_pipeline_stats: the ctypes mirror btsha1.PipelineStats has the
+    C struct's size and field offsets (compiled here against
+    include/bt_sha1.h), and a thread that has run no host pipeline gets -1
+    with a message, not stale numbers."""
+    import threading
+    bt = load_btsha1()
+    fields = [f for f, _ in bt.PipelineStats._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "bt_sha1.h"\nint main(void) {\n'
+                   '  printf("size %zu\\n", sizeof(bt_sha1_pipeline_stats));\n'
+                   + "".join(f'  printf("{f} %zu\\n", offsetof(bt_sha1_pipeline_stats, {f}));\n' for f in fields)
+                   + "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), "-o", str(exe), str(src)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True, check=True)
+               .stdout.splitlines())
+    assert int(got["size"]) == ctypes.sizeof(bt.PipelineStats)
+    for f in fields:
+        assert int(got[f]) == getattr(bt.PipelineStats, f).offset, f
+    err = []
+
+    def fresh_thread():
+        try:
+            bt.pipeline_stats()
+        except bt.BtSha1Error as e:
+            err.append(str(e))
+    t = threading.Thread(target=fresh_thread)
+    t.start()
+    t.join()
+    assert err and "no host pipeline has run on this thread" in err[0]
+
+
 EXP_LIB = os.path.join(REPO, "build_variants", "experiments", "libbtsha1.so")
 
 

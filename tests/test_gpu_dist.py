@@ -114,7 +114,7 @@ def _check_sample(line, world, chunks, oracle):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_ranks_split_and_gather_on_one_gpu(world, oracle):
     chunks = 4096 // world
-    line = _run_bench(world, chunks)
+    line = _run_bench(world, chunks, "--no-cpu-baseline")
     assert line["n_gpus"] == world and line["steps"] == 3 and line["warmup"] == 1
     assert line["config"]["global_chunks"] == 4096
     assert line["parity_first_4096_vs_golden"] is True
@@ -127,7 +127,8 @@ def test_bench_ranks_split_and_gather_on_one_gpu(world, oracle):
     assert all(abs(p["kernel_GiB_per_s"] * p["kernel_ms"] * 1e-3 * 2**30 - chunks * CHUNK) < 1e-3 * chunks * CHUNK
                for p in line["per_gpu"])
     assert line["value"] > 0 and line["scaling"] == "weak"
-    # N > 1: no CPU baseline / host-path legs (rank 0 at N = 1 only)
+    # N > 1: no host-path leg (rank 0 at N = 1 only); the CPU baseline was
+    # switched off here (test_bench_gpus_flag_alone_starts_the_ranks runs it)
     assert line["cpu_baseline"] is None and line["host_path"] is None
     # every rank read its own GPU's board power after the timed region
     assert [p["rank"] for p in line["power"]["per_gpu"]] == list(range(world))
@@ -144,7 +145,7 @@ def test_bench_ranks_run_the_hot_kernel_with_parity_on_every_rank(oracle, world,
     ranks x 40960 (160 GiB on the one GPU) is the driver's N = 8 launch with
     every rank on the hot kernel: 327,680 digests, all compared with the
     reference's checksum and with the oracle."""
-    line = _run_bench(world, chunks, "--power-s", "0", timeout=300)
+    line = _run_bench(world, chunks, "--power-s", "0", "--no-cpu-baseline", timeout=300)
     assert line["roofline"]["kernel"] == "k_sha1_fixed"
     assert line["config"]["global_chunks"] == world * chunks
     assert line["parity_first_4096_vs_golden"] is True   # rank 0's first 4096 vs sha.c golden
@@ -172,9 +173,16 @@ def test_bench_gpus_flag_alone_starts_the_ranks(oracle, world, chunks):
     shape): bench.py starts the N ranks itself and relays rank 0's one line
     -- n_gpus N, N per_gpu entries, every digest equal to the reference's
     checksum (81,920 chunks on the hot kernel with per-rank clocks; 8 ranks x
-    512 chunks = config 2's 4096 on the latency kernel)."""
+    512 chunks = config 2's 4096 on the latency kernel) -- and, as every
+    N > 1 SCALE line must (north_star: "next to the reference sha.c timed on
+    the GPU box's own host cores in the same run"), rank 0's CPU baseline:
+    the reference's own sha.c, its digests equal to the GPU's."""
     line = _run_bench(world, chunks, "--power-s", "0", launcher=False, timeout=300)
     assert line["n_gpus"] == world and len(line["per_gpu"]) == world
+    cpu = line["cpu_baseline"]
+    assert cpu["kind"] == "reference" and cpu["digests_match_gpu"] is True, cpu
+    assert cpu["value"] > 0 and cpu["cores"] >= 1 and "O2_1t" in cpu["runs"]
+    assert line["host_path"] is None and line["phases_s"]["cpu_baseline_s"] > 0
     assert line["config"]["global_chunks"] == world * chunks
     assert line["parity_all_vs_golden"] is True and line["parity_first_4096_vs_golden"] is True
     _check_identity(line, world, chunks)
@@ -221,3 +229,46 @@ def test_bench_single_rank_line_checks(oracle):
     assert o["min"] <= o["median"] <= o["max"]
     assert line["rehearse_shared_gpu"] is False and line["distinct_gpus"] == 1
     _check_sample(line, 1, 4096, oracle)
+
+
+def test_bench_host_path_leg_explains_itself(oracle):
+    """Config 5 in the N = 1 line (a 1 GiB image here): each pipeline rate is
+    the median of 5 steady-state runs after a first one, every run listed
+    with its phase split (host staging vs blocked on the GPU lane), the
+    pageable run's NUMA placement (GPU node, image / staging pages and
+    staging threads per node) and cgroup throttling; the batched verifier is
+    fed zero-copy and packetized (util.c:275's 1484-byte memcpys) on one and
+    on four receive threads -- every digest and verdict right."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--chunks", "4096", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline", "--host-gib", "1", "--power-s", "0", "--no-clock"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    hp = line["host_path"]
+    assert hp["image_GiB"] == 1.0
+    for key in ("pageable_chunks_host", "registered_direct_dma"):
+        p = hp[key]
+        assert p["digests_match"] is True and len(p["runs"]) == 6, p
+        steady = sorted(x["GiB_per_s"] for x in p["runs"][1:])
+        assert p["GiB_per_s"] == round(steady[2], 3) and p["steady_min_max"] == [steady[0], steady[-1]]
+        for run in p["runs"]:
+            assert run["s"] > 0 and run["wait_s"] >= 0 and run["fill_s"] >= 0 and run["cpu_s"] >= 0
+            assert run["fill_s"] + run["wait_s"] <= run["s"] * 1.05 + 1e-3
+        ph = p["median_run_phases"]
+        assert 0 <= ph["fill_frac"] <= 1.05
+    pg = hp["pageable_chunks_host"]
+    numa = pg["numa"]
+    assert numa["numa_nodes"] >= 1 and len(numa["image_pages_per_node"]) == numa["numa_nodes"]
+    assert sum(numa["image_pages_per_node"]) > 0 and sum(numa["lane_pages_per_node"]) > 0
+    assert sum(numa["staging_pieces_per_cpu_node"]) > 0
+    if numa["policy"] == "gpu":  # the lanes and the staging threads sit on the GPU's node
+        g = numa["gpu_node"]
+        assert numa["lane_pages_per_node"][g] == sum(numa["lane_pages_per_node"])
+        assert numa["staging_pieces_per_cpu_node"][g] == sum(numa["staging_pieces_per_cpu_node"])
+    assert 0 < pg["frac_of_raw_h2d"] < 1.2
+    for key, threads in (("zero_copy_verifier", 1), ("packetized_verifier", 1), ("packetized_verifier_4_threads", 4)):
+        v = hp[key]
+        assert v["digests_match"] is True and v["GiB_per_s"] > 0 and "error" not in v, (key, v)
+        assert v["receive_threads"] == threads
+    assert hp["packetized_verifier"]["timed_chunks"] == 2 * 2048

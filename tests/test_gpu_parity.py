@@ -8,6 +8,7 @@ import os
 import random
 import subprocess
 import threading
+import time
 
 import pytest
 
@@ -576,6 +577,42 @@ def test_full_size_config3_properties(bt, torch, oracle):
     assert not bad, (len(bad), bad[:10])
 
 
+def test_pipeline_stats_account_for_each_host_run(bt, oracle, tmp_path):
+    """bt_sha1_get_pipeline_stats after each kind of host pipeline run on
+    this thread: chunk and byte counts, batches, staged or direct DMA, a
+    phase split that fits inside the call, and the NUMA placement (under the
+    default policy on a multi-node box the staging lanes and the staging
+    threads sit on the GPU's node)."""
+    import numpy as np
+    data = np.frombuffer(bytes(oracle.fill_synthetic(150 * CHUNK + 999, 7, 0x57A7)), dtype=np.uint8).copy()
+    want = b"".join(oracle.hash_chunks(bytes(data), CHUNK))
+    addr = data.ctypes.data
+    t0 = time.perf_counter()
+    assert bt.chunks_host_addr(addr, data.nbytes) == want
+    wall = time.perf_counter() - t0
+    s = bt.pipeline_stats()
+    assert (s["chunks"], s["bytes"], s["staged"]) == (151, data.nbytes, True)
+    assert s["batches"] == 2 and s["batch_bytes"] == 76 * CHUNK  # a 64 MiB - 2 GiB input: two batches
+    assert 0 < s["total_s"] <= wall and s["fill_s"] + s["wait_s"] + s["alloc_s"] <= s["total_s"] * 1.001
+    assert sum(s["src_pages"]) > 0 and sum(s["lane_pages"]) > 0 and sum(s["copy_pieces"]) > 0
+    if s["numa_policy"] == "gpu":
+        g = s["gpu_numa_node"]
+        assert s["lane_pages"][g] == sum(s["lane_pages"]) and s["copy_pieces"][g] == sum(s["copy_pieces"])
+    bt.host_register(addr, data.nbytes)
+    try:
+        assert bt.chunks_host_addr(addr, data.nbytes) == want
+        d = bt.pipeline_stats()
+        assert (d["chunks"], d["staged"], d["numa_policy"]) == (151, False, "none")
+        assert sum(d["copy_pieces"]) == 0 and sum(d["lane_pages"]) == 0
+    finally:
+        bt.host_unregister(addr)
+    f = tmp_path / "img"
+    f.write_bytes(data.tobytes())
+    assert b"".join(bt.make_chunks_file(str(f))) == want
+    m = bt.pipeline_stats()
+    assert (m["chunks"], m["bytes"], m["staged"]) == (151, data.nbytes, True)
+
+
 def test_registered_host_image_direct_dma(bt, oracle):
     import numpy as np
     data = np.frombuffer(bytes(oracle.fill_synthetic(9 * CHUNK + 777, 5, 0xD1A), ), dtype=np.uint8).copy()
@@ -645,6 +682,38 @@ def test_verify_stream_chunks_dealt_modulo_g_verifiers(tmp_path, oracle, g):
     assert r.returncode == 0, (r.stdout[-500:], r.stderr[-500:])
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert (summary["chunks"], summary["ok"], summary["failed"]) == (3 * 12 * g, 3 * 12 * g, 0)
+
+
+@pytest.mark.parametrize("g", [2, 4])
+def test_verify_stream_receive_threads_and_warmup_rounds(tmp_path, oracle, g):
+    """-t: every verifier gets a receive thread of its own (the packetized
+    util.c:275 copies of the G verifiers run side by side); -w: untimed
+    warm-up rounds.  Every 7th chunk corrupted (-x) fails in every round,
+    exactly those; the summary counts the timed rounds only."""
+    exe = os.path.join(PKG, "bin", "verify-stream")
+    n = 8 * g
+    img = bytes(oracle.fill_synthetic(n * CHUNK, 17, 0xFEED))
+    p = tmp_path / "img"
+    p.write_bytes(img)
+    ck = tmp_path / "img.chunks"
+    ck.write_text("".join(f"{i} {d.hex()}\n" for i, d in enumerate(oracle.hash_chunks(img, CHUNK))))
+    r = subprocess.run([exe, "-g", str(g), "-t", "-b", "3", "-s", "2", "-r", "3", "-w", "1", "-x", str(p), str(ck)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout[-500:], r.stderr[-500:])
+    s = json.loads(r.stdout.strip().splitlines()[-1])
+    bad = 3 * sum(1 for k in range(n) if k % 7 == 3)
+    assert (s["chunks"], s["ok"], s["failed"], s["verifiers"], s["receive_threads"]) == (3 * n, 3 * n - bad, bad, g, g)
+    assert (s["timed_chunks"], s["warmup_rounds"], s["late_fills"]) == (2 * n, 1, 0)
+    assert r.stdout.count("Verification failed!") == bad
+    # zero-copy with receive threads: every commit of every ring verifies
+    r = subprocess.run([exe, "-g", str(g), "-t", "-z", "-b", "4", "-s", "2", "-r", "4", str(p), str(ck)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout[-500:], r.stderr[-500:])
+    s = json.loads(r.stdout.strip().splitlines()[-1])
+    assert (s["chunks"], s["ok"], s["failed"], s["timed_chunks"]) == (4 * 8 * g, 4 * 8 * g, 0, 3 * 8 * g)
+    # no timed round left: refused before any GPU work
+    r = subprocess.run([exe, "-r", "2", "-w", "2", str(p), str(ck)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 255 and "no timed round" in r.stderr
 
 
 def test_verifier_concurrent_downloads_out_of_order(bt):

@@ -166,7 +166,7 @@ def test_rank_identities_gathered_and_shared_gpu_refused(shared, allow):
         assert [i["chunk_range"] for i in idents] == [[0, 131072], [131072, 262144]]
         assert distinct == (1 if shared else 2)
         if shared and not allow:
-            assert clash and "0000:05:00.0 on box <- ranks [0, 1]" in clash and "--rehearse-shared-gpu" in clash
+            assert clash and "0000:05:00 on box <- ranks [0, 1]" in clash and "--rehearse-shared-gpu" in clash
         else:
             assert clash is None
 
@@ -192,9 +192,56 @@ def test_distinct_device_guard_logic():
     # two nodes x 4 ranks: equal PCI addresses on different hosts are different GPUs
     two = ids(full[:4] * 2, 8, hosts=["n0"] * 4 + ["n1"] * 4)
     assert shard.check_distinct_devices(two, 8) is None and shard.distinct_devices(two) == 8
-    # UUIDs only split keys: same address + host but different UUIDs -> distinct
-    parts = [{"rank": r, "host": "n0", "pci_bdf": full[0], "uuid": f"u{r}"} for r in range(2)]
+    # UUIDs from one source only split keys: same address + host, different UUIDs -> distinct
+    parts = [{"rank": r, "host": "n0", "pci_bdf": full[0], "uuid": f"u{r}", "uuid_source": "smi"} for r in range(2)]
     assert shard.check_distinct_devices(parts, 2) is None
+
+
+def _smi_ident(rank, smi_bdf, uuid="54ff75a3-0000-1000-806c-9eb5603801dc", hip_bdf=None):
+    """A rank whose amdsmi lookup worked: amdsmi's full address (with the
+    function number) beside HIP's (function fixed at .0), amdsmi's UUID."""
+    return {"rank": rank, "host": "n0", "pci_bdf": hip_bdf or smi_bdf.rsplit(".", 1)[0] + ".0",
+            "smi_bdf": smi_bdf, "uuid": uuid, "uuid_source": "smi", "device_count": 1}
+
+
+def test_gpu_identity_keys_on_the_full_pci_address():
+    """Partitions of one GPU differ only in the PCI function number, which HIP
+    does not report (bench.py builds pci_bdf with .0): with amdsmi's address
+    on every rank, ...:00.0 and ...:00.1 are two devices, and two ranks at one
+    smi_bdf are refused.  Spellings are normalised (case, domain)."""
+    shard = _load_shard()
+    two = [_smi_ident(0, "0000:5d:00.0", "u-a"), _smi_ident(1, "0000:5d:00.1", "u-b")]
+    assert two[0]["pci_bdf"] == two[1]["pci_bdf"] == "0000:5d:00.0"
+    assert shard.check_distinct_devices(two, 2) is None and shard.distinct_devices(two) == 2
+    # the same UUID (one physical package) does not merge two functions either
+    same_pkg = [_smi_ident(0, "0000:5d:00.0"), _smi_ident(1, "0000:5d:00.1")]
+    assert shard.check_distinct_devices(same_pkg, 2) is None
+    one = [_smi_ident(0, "0000:5d:00.1"), _smi_ident(1, "0000:5D:00.1")]
+    msg = shard.check_distinct_devices(one, 2)
+    assert msg and "0000:5d:00.1 on n0 <- ranks [0, 1]" in msg and shard.distinct_devices(one) == 1
+
+
+def test_gpu_identity_never_splits_one_gpu_over_two_sources():
+    """amdsmi and HIP spell one GPU's UUID differently, and only
+    amdsmi gives the function number.  A launch where amdsmi failed on some
+    ranks of a shared GPU must still be refused: every rank is then keyed on
+    the coarser address (domain:bus:device) and no UUID."""
+    shard = _load_shard()
+    smi = _smi_ident(0, "0000:5d:00.0")
+    hip = {"rank": 1, "host": "n0", "pci_bdf": "0000:5d:00.0", "uuid": "GPU-9eb5603801dc", "uuid_source": "hip",
+           "smi_error": "AmdSmiLibraryException", "device_count": 1}
+    msg = shard.check_distinct_devices([smi, hip], 2)
+    assert msg and "ranks [0, 1]" in msg and shard.distinct_devices([smi, hip]) == 1
+    # ... also when the amdsmi rank sits on function 1 of the same device
+    smi1 = _smi_ident(0, "0000:5d:00.1")
+    assert shard.check_distinct_devices([smi1, hip], 2)
+    # both ranks on HIP's fields alone: one source, so its UUIDs may split
+    hip0 = dict(hip, rank=0, uuid="GPU-a")
+    assert shard.check_distinct_devices([hip0, hip], 2) is None
+    assert shard.check_distinct_devices([hip0, dict(hip, uuid="GPU-a")], 2)
+    # distinct GPUs stay distinct under the coarse key
+    other = dict(hip, pci_bdf="0000:75:00.0")
+    assert shard.check_distinct_devices([smi, other], 2) is None
 
 
 def test_bench_uses_the_shard_protocol():

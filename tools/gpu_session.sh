@@ -234,6 +234,17 @@ for step in "$@"; do
         run "co_overlap_$rep" 600 env BT_SHA1_COPY_ORDER=overlap python3 tools/numa_probe.py 8 && \
         run "co_serial_$rep" 600 env BT_SHA1_COPY_ORDER=serial python3 tools/numa_probe.py 8 || exit 1
       done ;;
+    numa_place)
+      # round 6: staging placement (lanes + copy threads on the GPU's node, or
+      # left to the kernel) x image node, alternating, median of 5 runs each
+      for rep in 1 2; do
+        run "np_gpu_$rep" 300 env BT_SHA1_NUMA=gpu python3 tools/numa_probe.py 8 5 && \
+        run "np_off_$rep" 300 env BT_SHA1_NUMA=off python3 tools/numa_probe.py 8 5 || exit 1
+      done ;;
+    copythreads)
+      for t in 8 16 4 12; do
+        run "ct_$t" 300 env BT_SHA1_COPY_THREADS=$t python3 tools/numa_probe.py 8 5 || exit 1
+      done ;;
     latency_ab)
       run latency_spin 300 python3 tools/latency_bench.py
       run latency_streamsync 300 env BT_SHA1_SYNC=stream python3 tools/latency_bench.py

@@ -596,6 +596,18 @@ def cgroup_cpu_stat():
         return None
 
 
+def machine_cpu_ticks():
+    """(busy, total) jiffies of the whole machine (/proc/stat `cpu` line: not
+    namespaced, so it counts every tenant of the host, not only this job)."""
+    try:
+        with open("/proc/stat") as f:
+            v = [int(x) for x in f.readline().split()[1:]]
+        idle = v[3] + (v[4] if len(v) > 4 else 0)
+        return sum(v) - idle, sum(v)
+    except (OSError, ValueError, IndexError):
+        return None
+
+
 def timed_runs(fn, want, gib, steady=5, stats=None):
     """The first run of a host path (it also pays one-time pinning), then
     `steady` more; value = the MEDIAN steady run.  Every run is listed with
@@ -606,15 +618,17 @@ def timed_runs(fn, want, gib, steady=5, stats=None):
     import statistics
     runs, ok = [], True
     for _ in range(1 + steady):
-        cg0, cpu0 = cgroup_cpu_stat(), time.process_time()
+        cg0, cpu0, m0 = cgroup_cpu_stat(), time.process_time(), machine_cpu_ticks()
         t0 = time.perf_counter()
         r = fn()
         dt = time.perf_counter() - t0
-        cpu, cg1 = time.process_time() - cpu0, cgroup_cpu_stat()
+        cpu, cg1, m1 = time.process_time() - cpu0, cgroup_cpu_stat(), machine_cpu_ticks()
         ok = ok and r == want
         row = {"GiB_per_s": round(gib / dt, 3), "s": round(dt, 4), "cpu_s": round(cpu, 3)}
         if cg0 and cg1:
             row["cgroup_throttled_s"] = round(cg1["throttled_s"] - cg0["throttled_s"], 4)
+        if m0 and m1 and m1[1] > m0[1]:
+            row["machine_cpu_busy"] = round((m1[0] - m0[0]) / (m1[1] - m0[1]), 3)
         if stats is not None:
             s = stats()
             row.update(fill_s=s["fill_s"], wait_s=s["wait_s"], alloc_s=s["alloc_s"],

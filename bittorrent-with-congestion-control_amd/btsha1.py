@@ -327,7 +327,7 @@ def pipeline_stats():
         d[k] = list(d[k])[:nodes]
     for k in ("total_s", "alloc_s", "fill_s", "wait_s"):
         d[k] = round(d[k], 4)
-    d["staged"], d["numa_policy"] = bool(s.staged), ("gpu" if s.numa_policy else "none")
+    d["staged"], d["numa_policy"] = bool(s.staged), {1: "lanes", 2: "gpu"}.get(s.numa_policy, "none")
     return d
 
 

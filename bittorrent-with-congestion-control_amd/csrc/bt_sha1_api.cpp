@@ -211,14 +211,22 @@ int gpu_numa_node(int dev) {
   return node;
 }
 
-// BT_SHA1_NUMA=off disables the placement; default (or "gpu"): place when the
-// machine has more than one node and the GPU's node is known.
-bool numa_placement_wanted() {
-  static const bool on = [] {
+// Staging placement (BT_SHA1_NUMA): "off" = none (pages wherever the kernel
+// puts them, copy threads unpinned); "lanes" = the lanes' pages prefer the
+// GPU's node; "gpu" = that, and the copy threads run on the node's CPUs.
+// Applies only when the machine has more than one node and the GPU's node is
+// known.
+enum NumaMode { kNumaOff = 0, kNumaLanes = 1, kNumaGpu = 2 };
+constexpr int kNumaDefault = kNumaOff;
+int numa_mode() {
+  static const int m = [] {
     const char *e = getenv("BT_SHA1_NUMA");
-    return !(e && (!strcmp(e, "off") || !strcmp(e, "0")));
+    if (!e || !*e) return (int)kNumaDefault;
+    if (!strcmp(e, "off") || !strcmp(e, "0")) return (int)kNumaOff;
+    if (!strcmp(e, "lanes")) return (int)kNumaLanes;
+    return (int)kNumaGpu;
   }();
-  return on;
+  return m;
 }
 
 // Pages of [p, p+len) sampled evenly (at most `samples`), counted per node
@@ -243,13 +251,19 @@ struct Placement {
   int node = -1;      // -1: no placement
   int ncpus = 0;      // 0: threads unpinned
   cpu_set_t cpus;
+  int mode() const { return node < 0 ? kNumaOff : ncpus > 0 ? kNumaGpu : kNumaLanes; }
 };
 
 Placement placement_for(int gpu_node) {
   Placement pl;
   CPU_ZERO(&pl.cpus);
   const NumaTopo &t = numa_topo();
-  if (!numa_placement_wanted() || gpu_node < 0 || t.nodes < 2 || gpu_node >= (int)t.node_cpus.size()) return pl;
+  const int mode = numa_mode();
+  if (mode == kNumaOff || gpu_node < 0 || t.nodes < 2 || gpu_node >= (int)t.node_cpus.size()) return pl;
+  if (mode == kNumaLanes) {
+    pl.node = gpu_node;
+    return pl;
+  }
   cpu_set_t aff;
   CPU_ZERO(&aff);
   if (sched_getaffinity(0, sizeof aff, &aff) != 0) return pl;
@@ -623,7 +637,16 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-constexpr uint64_t kPiece = 128ull << 20;  // staging -> H2D granule inside a batch
+// Staging -> H2D granule inside a batch: 128 MiB (BT_SHA1_PIECE_MB overrides,
+// 16 .. 1024).
+uint64_t piece_bytes() {
+  static const uint64_t v = [] {
+    const char *e = getenv("BT_SHA1_PIECE_MB");
+    const long mb = e ? atol(e) : 128;
+    return (uint64_t)(mb < 16 ? 16 : (mb > 1024 ? 1024 : mb)) << 20;
+  }();
+  return v;
+}
 
 // Copy order of the two lanes.  "serial": a batch's first H2D waits for the
 // previous batch's last one, so one copy runs at a time (hashing still
@@ -743,7 +766,7 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
       // Staged input moves in pieces (host reads overlap the H2D); pinned
       // input goes as one copy per batch -- 128 MiB copies straight from
       // registered memory measured 36.5 GiB/s against 50 for 1 GiB ones.
-      const uint64_t want = std::min<uint64_t>(staged ? kPiece : bytes_per, bytes_per - got);
+      const uint64_t want = std::min<uint64_t>(staged ? piece_bytes() : bytes_per, bytes_per - got);
       const uint8_t *src = nullptr;
       const double t0 = now_s();
       const int64_t r = fill(l, got, want, &src);
@@ -803,7 +826,7 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   s.copy_threads = copy_threads();
   s.numa_nodes = numa_topo().nodes;
   s.gpu_numa_node = c->numa_node;
-  s.numa_policy = place.node >= 0 ? 1 : 0;
+  s.numa_policy = place.mode();
   s.total_s = total;
   s.alloc_s = t_alloc;
   s.fill_s = t_fill;

@@ -184,11 +184,12 @@ int64_t bt_sha1_chunks_file(void *fp /* FILE* */, uint64_t chunk_len, uint8_t *h
  * means PCIe / the GPU do.  NUMA fields (Linux sysfs + move_pages): the
  * GPU's node, sampled pages of the staging lanes and of the caller's input
  * per node, and the staging pieces by the node of the CPU their thread ran
- * on; -1 / zeros where unknown.  numa_policy: 1 when the lanes were placed
- * on the GPU's node and the staging threads ran on that node's CPUs within
- * the caller's affinity mask (BT_SHA1_NUMA=gpu, the default when the GPU's
- * node is known and the machine has more than one node), 0 when not
- * (BT_SHA1_NUMA=off, one node, or no usable CPU of the GPU's node).
+ * on; -1 / zeros where unknown.  numa_policy (BT_SHA1_NUMA, applied only
+ * when the machine has more than one node and the GPU's node is known):
+ * 0 = none (the default: pages where the kernel puts them, staging threads
+ * unpinned), 1 = "lanes" (the staging lanes prefer the GPU's node), 2 =
+ * "gpu" (that, and the staging threads run on the node's CPUs within the
+ * caller's affinity mask).
  * Returns 0, or -1 when this thread has run no pipeline. */
 #define BT_SHA1_STATS_NODES 8
 typedef struct {
@@ -201,7 +202,7 @@ typedef struct {
   int32_t copy_threads;     /* staging threads per piece (BT_SHA1_COPY_THREADS) */
   int32_t numa_nodes;       /* NUMA nodes of the machine (sysfs)              */
   int32_t gpu_numa_node;    /* the GPU's node (-1: unknown)                   */
-  int32_t numa_policy;      /* see above                                      */
+  int32_t numa_policy;      /* 0 none, 1 lanes, 2 lanes + threads (see above) */
   int32_t reserved;
   double total_s;           /* the whole call                                 */
   double alloc_s;           /* lane allocation / page-locking in the call     */

@@ -235,15 +235,21 @@ for step in "$@"; do
         run "co_serial_$rep" 600 env BT_SHA1_COPY_ORDER=serial python3 tools/numa_probe.py 8 || exit 1
       done ;;
     numa_place)
-      # round 6: staging placement (lanes + copy threads on the GPU's node, or
-      # left to the kernel) x image node, alternating, median of 5 runs each
+      # round 6: staging placement (off: left to the kernel; lanes: the lanes'
+      # pages on the GPU's node; gpu: lanes + copy threads there) x image node,
+      # alternating, median of 5 runs each
       for rep in 1 2; do
-        run "np_gpu_$rep" 300 env BT_SHA1_NUMA=gpu python3 tools/numa_probe.py 8 5 && \
-        run "np_off_$rep" 300 env BT_SHA1_NUMA=off python3 tools/numa_probe.py 8 5 || exit 1
+        for m in off lanes gpu; do
+          run "np_${m}_$rep" 300 env BT_SHA1_NUMA=$m python3 tools/numa_probe.py 8 5 || exit 1
+        done
       done ;;
     copythreads)
-      for t in 8 16 4 12; do
+      for t in 16 12 8 16 12 8; do
         run "ct_$t" 300 env BT_SHA1_COPY_THREADS=$t python3 tools/numa_probe.py 8 5 || exit 1
+      done ;;
+    pieces)
+      for mb in 64 256 128 64 256 128; do
+        run "pc_$mb" 300 env BT_SHA1_PIECE_MB=$mb python3 tools/numa_probe.py 8 5 || exit 1
       done ;;
     latency_ab)
       run latency_spin 300 python3 tools/latency_bench.py

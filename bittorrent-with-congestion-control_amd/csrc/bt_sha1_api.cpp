@@ -212,12 +212,16 @@ int gpu_numa_node(int dev) {
 }
 
 // Staging placement (BT_SHA1_NUMA): "off" = none (pages wherever the kernel
-// puts them, copy threads unpinned); "lanes" = the lanes' pages prefer the
-// GPU's node; "gpu" = that, and the copy threads run on the node's CPUs.
-// Applies only when the machine has more than one node and the GPU's node is
-// known.
+// puts them, copy threads unpinned); "lanes" (default) = the lanes' pages
+// prefer the GPU's node, so the DMA engine reads local memory; "gpu" = that,
+// and the copy threads run on the node's CPUs.  Applies only when the machine
+// has more than one node and the GPU's node is known.  Measured on MI355X
+// boxes (tools/numa_probe.py, profiles/r06/numa_place.md), 8 GiB images on
+// either node: off 49.0-50.4, lanes 50.1-50.5 GiB/s; pinning the copy
+// threads to the GPU node's cores cost 15-30 % on hosts whose cores other
+// jobs share (34.5-40.7 GiB/s), so it is not the default.
 enum NumaMode { kNumaOff = 0, kNumaLanes = 1, kNumaGpu = 2 };
-constexpr int kNumaDefault = kNumaOff;
+constexpr int kNumaDefault = kNumaLanes;
 int numa_mode() {
   static const int m = [] {
     const char *e = getenv("BT_SHA1_NUMA");

@@ -186,10 +186,11 @@ int64_t bt_sha1_chunks_file(void *fp /* FILE* */, uint64_t chunk_len, uint8_t *h
  * per node, and the staging pieces by the node of the CPU their thread ran
  * on; -1 / zeros where unknown.  numa_policy (BT_SHA1_NUMA, applied only
  * when the machine has more than one node and the GPU's node is known):
- * 0 = none (the default: pages where the kernel puts them, staging threads
- * unpinned), 1 = "lanes" (the staging lanes prefer the GPU's node), 2 =
- * "gpu" (that, and the staging threads run on the node's CPUs within the
- * caller's affinity mask).
+ * 0 = "off" (pages where the kernel puts them), 1 = "lanes" (the default:
+ * the staging lanes and the verifier's receive slots prefer the GPU's
+ * node), 2 = "gpu" (that, and the staging threads run on the node's CPUs
+ * within the caller's affinity mask -- measured 15-30 % slower on a shared
+ * host, where the node's cores are busy with other work: DESIGN.md §6).
  * Returns 0, or -1 when this thread has run no pipeline. */
 #define BT_SHA1_STATS_NODES 8
 typedef struct {

@@ -631,7 +631,7 @@ def timed_runs(fn, want, gib, steady=5, stats=None):
             row["machine_cpu_busy"] = round((m1[0] - m0[0]) / (m1[1] - m0[1]), 3)
         if stats is not None:
             s = stats()
-            row.update(fill_s=s["fill_s"], wait_s=s["wait_s"], alloc_s=s["alloc_s"],
+            row.update(fill_s=s["fill_s"], wait_s=s["wait_s"], alloc_s=s["alloc_s"], register_s=s["register_s"],
                        fill_GiB_per_s=round(gib / s["fill_s"], 2) if s["fill_s"] > 0 else None)
         runs.append(row)
     steady_rates = [r["GiB_per_s"] for r in runs[1:]]
@@ -647,8 +647,10 @@ def timed_runs(fn, want, gib, steady=5, stats=None):
 
 
 def numa_view(st):
-    """NUMA placement of a pipeline run, from bt_sha1_get_pipeline_stats."""
-    return {"numa_nodes": st["numa_nodes"], "gpu_node": st["gpu_numa_node"], "policy": st["numa_policy"],
+    """How a pipeline run was fed and where its memory sat, from
+    bt_sha1_get_pipeline_stats."""
+    return {"feed": st["feed"], "registered_batches": st["registered_batches"], "batches": st["batches"],
+            "numa_nodes": st["numa_nodes"], "gpu_node": st["gpu_numa_node"], "policy": st["numa_policy"],
             "image_pages_per_node": st["src_pages"], "lane_pages_per_node": st["lane_pages"],
             "staging_pieces_per_cpu_node": st["copy_pieces"], "copy_threads": st["copy_threads"],
             "method": "move_pages() over 64 sampled pages of the image / of each staging lane; staging pieces "
@@ -688,8 +690,21 @@ def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
     out["pageable_chunks_host"] = {
         **timed_runs(lambda: bt.chunks_host_addr(addr, nbytes), want, gib, stats=bt.pipeline_stats),
         "numa": numa_view(bt.pipeline_stats()),
-        "path": "bt_sha1_chunks_host on pageable memory: threaded staging memcpy into pinned lanes (on the "
-                "GPU's NUMA node), 2-stream H2D, hot kernel, digests to pinned host"}
+        "path": "bt_sha1_chunks_host on pageable memory (default feed): each ~1 GiB batch's whole pages "
+                "page-locked just ahead of its DMA and released after, unaligned edge bytes through a pinned "
+                "buffer, serial H2D on 2 streams, hot kernel, digests to pinned host"}
+    # The same call with the pre-round-6 feed: 8 threads copy every byte into
+    # page-locked staging lanes (on the GPU's NUMA node) ahead of the H2D --
+    # its rate follows the host's free memory bandwidth and cores.
+    prev = bt.set_pageable_feed("stage")
+    try:
+        out["pageable_staged_copy"] = {
+            **timed_runs(lambda: bt.chunks_host_addr(addr, nbytes), want, gib, stats=bt.pipeline_stats),
+            "numa": numa_view(bt.pipeline_stats()),
+            "path": "bt_sha1_chunks_host on pageable memory, BT_SHA1_PAGEABLE=stage: threaded staging memcpy "
+                    "into pinned lanes on the GPU's NUMA node, 2-stream H2D, hot kernel"}
+    finally:
+        bt.set_pageable_feed(prev)
     t0 = time.perf_counter()
     bt.host_register(addr, nbytes)
     reg_s = time.perf_counter() - t0
@@ -712,8 +727,8 @@ def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
                                   "path": "one hipMemcpy of the registered image (best of 3)"}
     finally:
         bt.host_unregister(addr)
-    pg = out["pageable_chunks_host"]
-    pg["frac_of_raw_h2d"] = round(pg["GiB_per_s"] / out["raw_h2d_ceiling"]["GiB_per_s"], 4)
+    for key in ("pageable_chunks_host", "pageable_staged_copy", "registered_direct_dma"):
+        out[key]["frac_of_raw_h2d"] = round(out[key]["GiB_per_s"] / out["raw_h2d_ceiling"]["GiB_per_s"], 4)
     # The batched verifier (util.c:304-337 replacement): the product's C host
     # tool over a 1 GiB image in a tmpfs file.  Zero-copy: the receive landed
     # the bytes in the pinned slots once, the timed rounds re-verify them (the

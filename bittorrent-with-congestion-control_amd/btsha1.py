@@ -47,9 +47,10 @@ class PipelineStats(ctypes.Structure):  # include/bt_sha1.h bt_sha1_pipeline_sta
     _fields_ = [("chunks", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64),
                 ("batches", ctypes.c_uint32), ("staged", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("copy_threads", ctypes.c_int32), ("numa_nodes", ctypes.c_int32),
-                ("gpu_numa_node", ctypes.c_int32), ("numa_policy", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("gpu_numa_node", ctypes.c_int32), ("numa_policy", ctypes.c_int32),
+                ("registered_batches", ctypes.c_int32),
                 ("total_s", ctypes.c_double), ("alloc_s", ctypes.c_double), ("fill_s", ctypes.c_double),
-                ("wait_s", ctypes.c_double),
+                ("wait_s", ctypes.c_double), ("register_s", ctypes.c_double),
                 ("lane_pages", ctypes.c_int32 * STATS_NODES), ("src_pages", ctypes.c_int32 * STATS_NODES),
                 ("copy_pieces", ctypes.c_int32 * STATS_NODES)]
 
@@ -86,6 +87,7 @@ _sig("bt_sha1_debug_barrier_stats", ctypes.c_int, ctypes.POINTER(ctypes.c_uint64
 _sig("bt_sha1_debug_dropin_residue", _i64, ctypes.c_int)
 _sig("bt_sha1_chunks_file", _i64, _vp, _u64, _vp, _u64)
 _sig("bt_sha1_get_pipeline_stats", ctypes.c_int, ctypes.POINTER(PipelineStats))
+_sig("bt_sha1_set_pageable_feed", ctypes.c_int, ctypes.c_int)
 _sig("bt_sha1_verifier_create", _vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32)
 _sig("bt_sha1_verifier_destroy", None, _vp)
 _sig("bt_sha1_verifier_slot", _vp, _vp)
@@ -315,6 +317,17 @@ def chunks_host_addr(addr, nbytes, chunk_len=CHUNK, ndev=None, devs=None):
     return bytes(out)[:20 * got]
 
 
+PAGEABLE_FEEDS = {"register": 0, "stage": 1}
+
+
+def set_pageable_feed(feed):
+    """How bt_sha1_chunks_host feeds pageable input >= 64 MiB: "register" (page-lock
+    batch by batch, DMA in place; the default) or "stage" (copy into the staging
+    lanes).  Returns the previous setting's name."""
+    prev = _check(lib.bt_sha1_set_pageable_feed(PAGEABLE_FEEDS[feed]), "bt_sha1_set_pageable_feed")
+    return {v: k for k, v in PAGEABLE_FEEDS.items()}[prev]
+
+
 def pipeline_stats():
     """Phase times and NUMA placement of this thread's last host pipeline run
     (bt_sha1_get_pipeline_stats) as a dict; per-node tallies are trimmed to
@@ -322,12 +335,13 @@ def pipeline_stats():
     s = PipelineStats()
     _check(lib.bt_sha1_get_pipeline_stats(ctypes.byref(s)), "bt_sha1_get_pipeline_stats")
     nodes = max(1, min(STATS_NODES, s.numa_nodes))
-    d = {k: getattr(s, k) for k, _ in PipelineStats._fields_ if k != "reserved"}
+    d = {k: getattr(s, k) for k, _ in PipelineStats._fields_}
     for k in ("lane_pages", "src_pages", "copy_pieces"):
         d[k] = list(d[k])[:nodes]
-    for k in ("total_s", "alloc_s", "fill_s", "wait_s"):
+    for k in ("total_s", "alloc_s", "fill_s", "wait_s", "register_s"):
         d[k] = round(d[k], 4)
-    d["staged"], d["numa_policy"] = bool(s.staged), {1: "lanes", 2: "gpu"}.get(s.numa_policy, "none")
+    d["feed"] = {0: "direct", 1: "staged", 2: "registered"}.get(s.staged, "?")
+    d["staged"], d["numa_policy"] = s.staged == 1, {1: "lanes", 2: "gpu"}.get(s.numa_policy, "none")
     return d
 
 

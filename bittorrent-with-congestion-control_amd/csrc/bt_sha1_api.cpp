@@ -350,9 +350,11 @@ struct Lane {
   hipEvent_t copied = nullptr;  // after the batch's last H2D (serial copy order)
   StageBuf h_in;  // staged input pieces, DMA'd to d_in
   PinBuf h_dig;   // the kernel stores digests straight into it
+  PinBuf h_edge;  // registered-batch mode: the batch's unaligned head / tail bytes
   DevBuf d_in;
   bool busy = false;
   uint64_t first = 0, count = 0;  // chunk range in flight
+  void *reg = nullptr;  // caller pages registered for the batch in flight (unregistered once it is done)
 };
 
 struct DevCtx {
@@ -418,6 +420,7 @@ void release_ctx(DevCtx *c) {
     l.ev = nullptr;
     l.h_in.release();
     l.h_dig.release();
+    l.h_edge.release();
     l.d_in.release();
   }
   c->s = nullptr;
@@ -625,10 +628,13 @@ int64_t parallel_pread(int fd, uint8_t *dst, uint64_t want, uint64_t pos) {
 // Generic double-buffered pipeline over two streams: batch k+1's H2D overlaps
 // batch k's hashing, and inside a batch each 128 MiB piece is copied to the
 // device as soon as it is staged, so host reads overlap the H2D.
-// fill(lane, off, max_bytes, &src) provides up to max_bytes of the image at
-// byte `off` of the lane's batch (staged at lane.h_in + off, or in place when
-// already pinned) and returns the byte count (< max_bytes only at the end);
-// sink(first_chunk, count, digests) receives digests in chunk order.
+// fill(lane, off, max_bytes, &src, &eof) provides up to max_bytes of the
+// image at byte `off` of the lane's batch (staged at lane.h_in + off, or in
+// place when the DMA engine can read it) and returns the byte count -- fewer
+// than max_bytes at a piece boundary of its own -- setting eof when no input
+// follows (a return of 0 is the end too); sink(first_chunk, count, digests)
+// receives digests in chunk order.  A fill may register caller pages for the
+// batch (lane.reg): they are unregistered once the lane's batch is done.
 // BT_SHA1_TRACE=1: per-phase wall times of each pipeline run on stderr.
 bool trace_on() {
   static const bool on = [] {
@@ -640,6 +646,8 @@ bool trace_on() {
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+
+constexpr uint64_t kPage = 4096;  // host page (registration granule)
 
 // Staging -> H2D granule inside a batch: 128 MiB (BT_SHA1_PIECE_MB overrides,
 // 16 .. 1024).
@@ -675,14 +683,29 @@ bool serial_copies(bool staged) {
 thread_local bt_sha1_pipeline_stats t_stats;
 thread_local bool t_stats_valid = false;
 
+// How a pipeline's input reaches the DMA engine.
+enum class Feed {
+  kStaged,     // copied (memcpy / pread) into the pinned staging lanes
+  kDirect,     // the caller's memory is pinned already: DMA'd in place
+  kRegistered  // pageable caller memory page-locked batch by batch (chunks_host_on)
+};
+
+// Registration time of the calling thread's current pipeline run (the
+// registered feed's fill adds to it; drain adds the unregistration).
+thread_local double t_register = 0;
+thread_local uint32_t t_registered_batches = 0;
+
 template <class Fill, class Sink>
-int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool staged, Fill fill, Sink sink) {
+int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed feed, Fill fill, Sink sink) {
   if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
     set_err("chunk_len must be in [1, 4 GiB)");
     return -1;
   }
+  const bool staged = feed == Feed::kStaged;
   const double t_start = now_s();
   double t_fill = 0, t_wait = 0;
+  t_register = 0;
+  t_registered_batches = 0;
   if (ensure_streams(c)) return -1;
   const uint64_t bytes_per = batch_bytes_for(chunk_len, size_hint, staged);
   const uint64_t per = bytes_per / chunk_len;
@@ -709,7 +732,8 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   // used: an input that fits one batch never pins the second lane's memory.
   auto prepare = [&](Lane &l) -> int {
     const double t0 = now_s();
-    if ((staged && l.h_in.ensure(bytes_per, place.node)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per))
+    if ((staged && l.h_in.ensure(bytes_per, place.node)) || l.d_in.ensure(bytes_per) || l.h_dig.ensure(20 * per) ||
+        (feed == Feed::kRegistered && l.h_edge.ensure(2 * kPage)))
       return -1;
     t_alloc += now_s() - t0;
     return 0;
@@ -749,11 +773,30 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
     if (pre_rc) set_err("%s", pre_err.c_str());
     return pre_rc;
   };
+  // Caller pages a fill registered for a batch stay registered until that
+  // batch's copies are done -- on every exit path, errors included.
+  struct UnregisterAtExit {
+    DevCtx *c;
+    ~UnregisterAtExit() {
+      for (auto &l : c->lane)
+        if (l.reg) {
+          (void)hipStreamSynchronize(l.s);
+          (void)hipHostUnregister(l.reg);
+          l.reg = nullptr;
+        }
+    }
+  } unregister_at_exit{c};
   auto drain = [&](Lane &l) -> int {
     if (!l.busy) return 0;
     const double t0 = now_s();
     BT_CK(hipEventSynchronize(l.ev));
     t_wait += now_s() - t0;
+    if (l.reg) {
+      const double t1 = now_s();
+      BT_CK(hipHostUnregister(l.reg));
+      l.reg = nullptr;
+      t_register += now_s() - t1;
+    }
     sink(l.first, l.count, l.h_dig.as<uint8_t>());
     l.busy = false;
     return 0;
@@ -766,22 +809,19 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
     if (k > 0 && serial_copies(staged)) BT_CK(hipStreamWaitEvent(l.s, c->lane[(k + 1) & 1].copied, 0));
     uint64_t got = 0;
     bool eof = false;
-    while (got < bytes_per) {
+    while (got < bytes_per && !eof) {
       // Staged input moves in pieces (host reads overlap the H2D); pinned
       // input goes as one copy per batch -- 128 MiB copies straight from
       // registered memory measured 36.5 GiB/s against 50 for 1 GiB ones.
       const uint64_t want = std::min<uint64_t>(staged ? piece_bytes() : bytes_per, bytes_per - got);
       const uint8_t *src = nullptr;
       const double t0 = now_s();
-      const int64_t r = fill(l, got, want, &src);
+      const int64_t r = fill(l, got, want, &src, &eof);
       t_fill += now_s() - t0;
       if (r < 0) return -1;
       if (r) BT_CK(hipMemcpyAsync(l.d_in.as<uint8_t>() + got, src, (size_t)r, hipMemcpyHostToDevice, l.s));
       got += (uint64_t)r;
-      if ((uint64_t)r < want) {
-        eof = true;
-        break;
-      }
+      if (r == 0) eof = true;
     }
     if (got == 0) break;
     if (serial_copies(staged)) BT_CK(hipEventRecord(l.copied, l.s));
@@ -825,7 +865,9 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   s.bytes = 0;
   s.batch_bytes = bytes_per;
   s.batches = (uint32_t)k;
-  s.staged = staged ? 1 : 0;
+  s.staged = feed == Feed::kStaged ? 1 : feed == Feed::kRegistered ? 2 : 0;
+  s.registered_batches = (int32_t)t_registered_batches;
+  s.register_s = t_register;
   s.device = c->dev;
   s.copy_threads = copy_threads();
   s.numa_nodes = numa_topo().nodes;
@@ -842,10 +884,34 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, bool sta
   if (trace_on())
     fprintf(stderr, "libbtsha1 pipeline dev %d: %llu chunks, batch %llu B, %s: total %.4f s = alloc %.4f + fill %.4f "
                     "+ wait %.4f + other\n",
-            c->dev, (unsigned long long)next, (unsigned long long)bytes_per, staged ? "staged" : "direct DMA",
-            total, t_alloc, t_fill, t_wait);
+            c->dev, (unsigned long long)next, (unsigned long long)bytes_per,
+            staged ? "staged" : feed == Feed::kRegistered ? "registered batch by batch" : "direct DMA", total, t_alloc,
+            t_fill, t_wait);
   return (int64_t)next;
 }
+
+// Pageable input to bt_sha1_chunks_host: page-lock it batch by batch and DMA
+// it in place (default), or copy it into the staging lanes
+// (BT_SHA1_PAGEABLE=stage).  The staging copy is host memory bandwidth and
+// CPU time -- 8 threads moving every byte once more -- so its rate follows
+// whatever else the host's cores and memory are doing (profiles/r06: 34-50
+// GiB/s on shared hosts); registering a 1 GiB batch's pages costs well under
+// its 20 ms DMA and hides behind the previous batch's copy, so the pageable
+// path runs at the registered-image rate.  Inputs under kRegisterMin stay
+// staged (a few ms of copying at most).
+constexpr uint64_t kRegisterMin = 64ull << 20;
+std::atomic<int> g_pageable_feed{-1};  // BT_SHA1_PAGEABLE_REGISTER / _STAGE; -1: not read yet
+int pageable_feed() {
+  int v = g_pageable_feed.load();
+  if (v < 0) {
+    const char *e = getenv("BT_SHA1_PAGEABLE");
+    const int env = (e && !strcmp(e, "stage")) ? BT_SHA1_PAGEABLE_STAGE : BT_SHA1_PAGEABLE_REGISTER;
+    g_pageable_feed.compare_exchange_strong(v, env);
+    v = g_pageable_feed.load();
+  }
+  return v;
+}
+bool register_pageable() { return pageable_feed() == BT_SHA1_PAGEABLE_REGISTER; }
 
 // own: a worker context of this call (repeated device ids); NULL = the
 // device's shared context.
@@ -860,21 +926,74 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
     return -1;
   }
   const bool pinned = is_pinned(h_in);
+  const Feed feed = pinned ? Feed::kDirect
+                    : (register_pageable() && total >= kRegisterMin) ? Feed::kRegistered
+                                                                      : Feed::kStaged;
   uint64_t off = 0;
-  auto fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src) -> int64_t {
-    const uint64_t n = std::min<uint64_t>(max, total - off);
-    if (pinned) {
+  // Registered feed, per batch [b0, b1) of the input: the whole pages inside
+  // it, [p0, p1), are page-locked for the batch and DMA'd in place; the head
+  // [b0, p0) and tail [p1, b1) -- under a page each, shared with the
+  // neighbouring batch's pages -- go through the lane's small pinned edge
+  // buffer.  Pages that cannot be registered (read-only, registered by the
+  // caller elsewhere) are staged through the lane instead.
+  uint64_t b1 = 0, p0 = 0, p1 = 0;
+  bool locked = false;
+  auto fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src, bool *eof) -> int64_t {
+    uint64_t n = std::min<uint64_t>(max, total - off);
+    if (feed == Feed::kDirect) {
       *src = h_in + off;  // DMA straight from the caller's pinned image
-    } else {
+    } else if (feed == Feed::kStaged) {
       parallel_copy(l.h_in.as<uint8_t>() + at, h_in + off, n);
       *src = l.h_in.as<uint8_t>() + at;
+    } else {
+      if (at == 0) {  // a new batch: lock its whole pages
+        b1 = off + n;
+        const uintptr_t base = (uintptr_t)h_in;
+        p0 = ((base + off + kPage - 1) & ~(uintptr_t)(kPage - 1)) - base;
+        p1 = ((base + b1) & ~(uintptr_t)(kPage - 1)) - base;
+        locked = false;
+        if (p1 > p0) {
+          const double t0 = now_s();
+          const hipError_t e = hipHostRegister((void *)(h_in + p0), (size_t)(p1 - p0), hipHostRegisterPortable);
+          t_register += now_s() - t0;
+          if (e == hipSuccess) {
+            l.reg = (void *)(h_in + p0);
+            locked = true;
+            ++t_registered_batches;
+          } else {
+            (void)hipGetLastError();  // staged below
+          }
+        } else {
+          p0 = p1 = b1;  // no whole page: the batch (< 2 pages) rides in the edge buffer
+        }
+      }
+      uint8_t *edge = l.h_edge.as<uint8_t>();
+      if (off < p0) {  // head, or a batch without a whole page
+        n = std::min<uint64_t>(n, p0 - off);
+        memcpy(edge, h_in + off, n);
+        *src = edge;
+      } else if (off < p1) {
+        n = std::min<uint64_t>(n, p1 - off);
+        if (locked) {
+          *src = h_in + off;
+        } else {
+          if (l.h_in.ensure(batch_bytes_for(chunk_len, total, false), -1)) return -1;
+          parallel_copy(l.h_in.as<uint8_t>() + at, h_in + off, n);
+          *src = l.h_in.as<uint8_t>() + at;
+        }
+      } else {  // tail
+        n = std::min<uint64_t>(n, b1 - off);
+        memcpy(edge + kPage, h_in + off, n);
+        *src = edge + kPage;
+      }
     }
     off += n;
+    *eof = off == total;
     return (int64_t)n;
   };
 
   auto sink = [&](uint64_t first, uint64_t count, const uint8_t *d) { memcpy(h_dig + 20 * first, d, 20 * count); };
-  const int64_t n = run_pipeline(c, chunk_len, total, !pinned, fill, sink);
+  const int64_t n = run_pipeline(c, chunk_len, total, feed, fill, sink);
   if (n >= 0 && t_stats_valid) {
     t_stats.bytes = total;
     page_nodes(h_in, total, 64, t_stats.src_pages, BT_SHA1_STATS_NODES);
@@ -898,7 +1017,7 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
   const bool regular = fstat(fileno(fp), &st) == 0 && S_ISREG(st.st_mode) && pos >= 0 && st.st_size >= pos;
   if (regular) hint = (uint64_t)(st.st_size - pos);
   uint64_t fpos = regular ? (uint64_t)pos : 0;
-  auto fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src) -> int64_t {
+  auto fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src, bool *eof) -> int64_t {
     uint8_t *dst = l.h_in.as<uint8_t>() + at;
     *src = dst;
     if (regular) {
@@ -910,6 +1029,7 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
         return -1;
       }
       fpos += (uint64_t)got;
+      *eof = (uint64_t)got < max;
       return got;
     }
     // Pipe or device: fread to EOF as chunk.c:20 does.
@@ -923,15 +1043,16 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
       set_err("fread failed");
       return -1;
     }
+    *eof = got < max;
     return (int64_t)got;
   };
   uint64_t bytes_in = 0;
-  auto counted_fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src) -> int64_t {
-    const int64_t r = fill(l, at, max, src);
+  auto counted_fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src, bool *eof) -> int64_t {
+    const int64_t r = fill(l, at, max, src, eof);
     if (r > 0) bytes_in += (uint64_t)r;
     return r;
   };
-  const int64_t n = run_pipeline(c, chunk_len, hint, true, counted_fill, sink);
+  const int64_t n = run_pipeline(c, chunk_len, hint, Feed::kStaged, counted_fill, sink);
   if (n >= 0 && t_stats_valid) t_stats.bytes = bytes_in;
   if (regular) {
     // Leave the stream where the reference's fread loop leaves it: at EOF,
@@ -1401,6 +1522,16 @@ int64_t bt_sha1_chunks_host_multi(const void *h_in, uint64_t total_len, uint64_t
   std::vector<int> devs(ndev);
   for (int g = 0; g < ndev; ++g) devs[g] = g;
   return bt_sha1_chunks_host_devices(h_in, total_len, chunk_len, h_digests, devs.data(), ndev);
+}
+
+int bt_sha1_set_pageable_feed(int feed) {
+  if (feed != BT_SHA1_PAGEABLE_REGISTER && feed != BT_SHA1_PAGEABLE_STAGE) {
+    set_err("pageable feed %d: BT_SHA1_PAGEABLE_REGISTER (0) or BT_SHA1_PAGEABLE_STAGE (1)", feed);
+    return -1;
+  }
+  const int prev = pageable_feed();
+  g_pageable_feed.store(feed);
+  return prev;
 }
 
 int bt_sha1_get_pipeline_stats(bt_sha1_pipeline_stats *out) {

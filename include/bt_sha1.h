@@ -191,24 +191,40 @@ int64_t bt_sha1_chunks_file(void *fp /* FILE* */, uint64_t chunk_len, uint8_t *h
  * node), 2 = "gpu" (that, and the staging threads run on the node's CPUs
  * within the caller's affinity mask -- measured 15-30 % slower on a shared
  * host, where the node's cores are busy with other work: DESIGN.md §6).
+ * Pageable input of at least 64 MiB to bt_sha1_chunks_host is page-locked
+ * batch by batch (the whole pages of each ~1 GiB batch, just before its DMA,
+ * released once its digests are out) and DMA'd in place; the unaligned head
+ * and tail bytes of each batch, and pages that cannot be locked, are staged
+ * (BT_SHA1_PAGEABLE=stage: stage everything).
  * Returns 0, or -1 when this thread has run no pipeline. */
+/* How bt_sha1_chunks_host feeds pageable input of at least 64 MiB to the
+ * GPU: page-locked batch by batch and DMA'd in place (REGISTER, the default)
+ * or copied into the pinned staging lanes (STAGE; also BT_SHA1_PAGEABLE=stage
+ * in the environment).  Process-wide; returns the previous setting or -1. */
+#define BT_SHA1_PAGEABLE_REGISTER 0
+#define BT_SHA1_PAGEABLE_STAGE 1
+int bt_sha1_set_pageable_feed(int feed);
 #define BT_SHA1_STATS_NODES 8
 typedef struct {
   uint64_t chunks;          /* digests produced                               */
   uint64_t bytes;           /* input bytes                                    */
   uint64_t batch_bytes;     /* bytes per lane batch                           */
   uint32_t batches;         /* lane batches launched                          */
-  int32_t staged;           /* 1: copied into the lanes; 0: direct DMA        */
+  int32_t staged;           /* 1: copied into the lanes; 0: direct DMA from
+                               pinned input; 2: pageable input page-locked
+                               batch by batch and DMA'd in place             */
   int32_t device;           /* HIP device                                     */
   int32_t copy_threads;     /* staging threads per piece (BT_SHA1_COPY_THREADS) */
   int32_t numa_nodes;       /* NUMA nodes of the machine (sysfs)              */
   int32_t gpu_numa_node;    /* the GPU's node (-1: unknown)                   */
   int32_t numa_policy;      /* 0 none, 1 lanes, 2 lanes + threads (see above) */
-  int32_t reserved;
+  int32_t registered_batches; /* batches DMA'd from caller pages locked for them */
   double total_s;           /* the whole call                                 */
   double alloc_s;           /* lane allocation / page-locking in the call     */
-  double fill_s;            /* host staging (memcpy / pread) on the host      */
+  double fill_s;            /* providing the input on the host: staging copies
+                               / reads, or registering the batch's pages      */
   double wait_s;            /* blocked on a lane's H2D + hash                 */
+  double register_s;        /* registering + unregistering caller pages       */
   int32_t lane_pages[BT_SHA1_STATS_NODES];  /* sampled staging pages per node */
   int32_t src_pages[BT_SHA1_STATS_NODES];   /* sampled input pages per node   */
   int32_t copy_pieces[BT_SHA1_STATS_NODES]; /* staging pieces per CPU node    */

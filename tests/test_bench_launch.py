@@ -95,6 +95,16 @@ def test_relay_keeps_the_childs_exit_status(capfd):
     assert b.relay(_stub("pass")) == 1
 
 
+def test_relay_reports_a_signal_death_as_128_plus_the_signal(capfd):
+    """A child killed by signal S has returncode -S; sys.exit(-S) would exit
+    256 - S, which reads as an ordinary error.  relay maps it to 128 + S."""
+    import signal
+    b = _bench()
+    assert b.exit_status(-signal.SIGTERM) == 143 and b.exit_status(-signal.SIGKILL) == 137
+    assert b.exit_status(0) == 0 and b.exit_status(3) == 3
+    assert b.relay(_stub("import os, signal; os.kill(os.getpid(), signal.SIGKILL)")) == 137
+
+
 def test_gpus_n_starts_n_ranks_through_torchrun():
     """No launcher, --gpus 2: bench.py starts torch.distributed.run with two
     ranks that run bench.py with WORLD_SIZE=2 == --gpus (plan "ranks", no
@@ -135,7 +145,7 @@ def test_relay_forwards_sigterm_and_the_ranks_die_with_it(tmp_path):
     cpid = int(pidfile.read_text())
     p.send_signal(signal.SIGTERM)
     rc = p.wait(timeout=60)
-    assert rc != 0  # the child's SIGTERM death is the launcher's status (negative: killed by signal)
+    assert rc == 128 + signal.SIGTERM  # the child's SIGTERM death, as a shell reports it
     with pytest.raises(ProcessLookupError):
         for _ in range(100):
             os.kill(cpid, 0)

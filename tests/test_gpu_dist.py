@@ -234,11 +234,13 @@ def test_bench_single_rank_line_checks(oracle):
 def test_bench_host_path_leg_explains_itself(oracle):
     """Config 5 in the N = 1 line (a 1 GiB image here): each pipeline rate is
     the median of 5 steady-state runs after a first one, every run listed
-    with its phase split (host staging vs blocked on the GPU lane), the
-    pageable run's NUMA placement (GPU node, image / staging pages and
-    staging threads per node) and cgroup throttling; the batched verifier is
-    fed zero-copy and packetized (util.c:275's 1484-byte memcpys) on one and
-    on four receive threads -- every digest and verdict right."""
+    with its phase split (providing the input on the host vs blocked on the
+    GPU lane, page registration), machine CPU load and cgroup throttling;
+    the pageable image is fed both ways -- page-locked batch by batch (the
+    default) and copied into the staging lanes -- each with its NUMA
+    placement; the batched verifier is fed zero-copy and packetized
+    (util.c:275's 1484-byte memcpys) on one and on four receive threads --
+    every digest and verdict right."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--chunks", "4096", "--steps", "2",
                         "--warmup", "1", "--no-cpu-baseline", "--host-gib", "1", "--power-s", "0", "--no-clock"],
@@ -247,7 +249,7 @@ def test_bench_host_path_leg_explains_itself(oracle):
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     hp = line["host_path"]
     assert hp["image_GiB"] == 1.0
-    for key in ("pageable_chunks_host", "registered_direct_dma"):
+    for key in ("pageable_chunks_host", "pageable_staged_copy", "registered_direct_dma"):
         p = hp[key]
         assert p["digests_match"] is True and len(p["runs"]) == 6, p
         steady = sorted(x["GiB_per_s"] for x in p["runs"][1:])
@@ -255,18 +257,17 @@ def test_bench_host_path_leg_explains_itself(oracle):
         for run in p["runs"]:
             assert run["s"] > 0 and run["wait_s"] >= 0 and run["fill_s"] >= 0 and run["cpu_s"] >= 0
             assert run["fill_s"] + run["wait_s"] <= run["s"] * 1.05 + 1e-3
-        ph = p["median_run_phases"]
-        assert 0 <= ph["fill_frac"] <= 1.05
-    pg = hp["pageable_chunks_host"]
-    numa = pg["numa"]
-    assert numa["numa_nodes"] >= 1 and len(numa["image_pages_per_node"]) == numa["numa_nodes"]
-    assert sum(numa["image_pages_per_node"]) > 0 and sum(numa["lane_pages_per_node"]) > 0
-    assert sum(numa["staging_pieces_per_cpu_node"]) > 0
-    if numa["policy"] == "gpu":  # the lanes and the staging threads sit on the GPU's node
-        g = numa["gpu_node"]
-        assert numa["lane_pages_per_node"][g] == sum(numa["lane_pages_per_node"])
-        assert numa["staging_pieces_per_cpu_node"][g] == sum(numa["staging_pieces_per_cpu_node"])
-    assert 0 < pg["frac_of_raw_h2d"] < 1.2
+        assert 0 <= p["median_run_phases"]["fill_frac"] <= 1.05
+        assert 0 < p["frac_of_raw_h2d"] < 1.2
+    reg, stg = hp["pageable_chunks_host"]["numa"], hp["pageable_staged_copy"]["numa"]
+    assert reg["feed"] == "registered" and reg["registered_batches"] == reg["batches"] == 2
+    assert sum(reg["staging_pieces_per_cpu_node"]) == 0
+    assert stg["feed"] == "staged" and stg["registered_batches"] == 0
+    assert stg["numa_nodes"] >= 1 and len(stg["image_pages_per_node"]) == stg["numa_nodes"]
+    assert sum(stg["image_pages_per_node"]) > 0 and sum(stg["lane_pages_per_node"]) > 0
+    assert sum(stg["staging_pieces_per_cpu_node"]) > 0
+    if stg["policy"] in ("lanes", "gpu"):  # the lanes sit on the GPU's node
+        assert stg["lane_pages_per_node"][stg["gpu_node"]] == sum(stg["lane_pages_per_node"])
     for key, threads in (("zero_copy_verifier", 1), ("packetized_verifier", 1), ("packetized_verifier_4_threads", 4)):
         v = hp[key]
         assert v["digests_match"] is True and v["GiB_per_s"] > 0 and "error" not in v, (key, v)

@@ -7,6 +7,7 @@ import json
 import os
 import random
 import subprocess
+import sys
 import threading
 import time
 
@@ -579,10 +580,11 @@ def test_full_size_config3_properties(bt, torch, oracle):
 
 def test_pipeline_stats_account_for_each_host_run(bt, oracle, tmp_path):
     """bt_sha1_get_pipeline_stats after each kind of host pipeline run on
-    this thread: chunk and byte counts, batches, staged or direct DMA, a
-    phase split that fits inside the call, and the NUMA placement (under the
-    default policy on a multi-node box the staging lanes and the staging
-    threads sit on the GPU's node)."""
+    this thread: chunk and byte counts, batches, how the input was fed
+    (pageable >= 64 MiB: page-locked batch by batch; pinned: direct DMA; a
+    file: staged reads), a phase split that fits inside the call, and the
+    NUMA placement (under the default policy on a multi-node box the staging
+    lanes sit on the GPU's node)."""
     import numpy as np
     data = np.frombuffer(bytes(oracle.fill_synthetic(150 * CHUNK + 999, 7, 0x57A7)), dtype=np.uint8).copy()
     want = b"".join(oracle.hash_chunks(bytes(data), CHUNK))
@@ -591,18 +593,16 @@ def test_pipeline_stats_account_for_each_host_run(bt, oracle, tmp_path):
     assert bt.chunks_host_addr(addr, data.nbytes) == want
     wall = time.perf_counter() - t0
     s = bt.pipeline_stats()
-    assert (s["chunks"], s["bytes"], s["staged"]) == (151, data.nbytes, True)
+    assert (s["chunks"], s["bytes"], s["feed"], s["staged"]) == (151, data.nbytes, "registered", False)
     assert s["batches"] == 2 and s["batch_bytes"] == 76 * CHUNK  # a 64 MiB - 2 GiB input: two batches
+    assert s["registered_batches"] == 2 and s["register_s"] >= 0
     assert 0 < s["total_s"] <= wall and s["fill_s"] + s["wait_s"] + s["alloc_s"] <= s["total_s"] * 1.001
-    assert sum(s["src_pages"]) > 0 and sum(s["lane_pages"]) > 0 and sum(s["copy_pieces"]) > 0
-    if s["numa_policy"] == "gpu":
-        g = s["gpu_numa_node"]
-        assert s["lane_pages"][g] == sum(s["lane_pages"]) and s["copy_pieces"][g] == sum(s["copy_pieces"])
-    bt.host_register(addr, data.nbytes)
+    assert sum(s["src_pages"]) > 0 and sum(s["copy_pieces"]) == 0   # nothing copied by the staging threads
+    bt.host_register(addr, data.nbytes)  # nothing of the call left registered
     try:
         assert bt.chunks_host_addr(addr, data.nbytes) == want
         d = bt.pipeline_stats()
-        assert (d["chunks"], d["staged"], d["numa_policy"]) == (151, False, "none")
+        assert (d["chunks"], d["feed"], d["numa_policy"], d["registered_batches"]) == (151, "direct", "none", 0)
         assert sum(d["copy_pieces"]) == 0 and sum(d["lane_pages"]) == 0
     finally:
         bt.host_unregister(addr)
@@ -610,7 +610,74 @@ def test_pipeline_stats_account_for_each_host_run(bt, oracle, tmp_path):
     f.write_bytes(data.tobytes())
     assert b"".join(bt.make_chunks_file(str(f))) == want
     m = bt.pipeline_stats()
-    assert (m["chunks"], m["bytes"], m["staged"]) == (151, data.nbytes, True)
+    assert (m["chunks"], m["bytes"], m["feed"]) == (151, data.nbytes, "staged")
+    assert sum(m["lane_pages"]) > 0 and sum(m["copy_pieces"]) > 0
+    if m["numa_policy"] in ("lanes", "gpu"):
+        assert m["lane_pages"][m["gpu_numa_node"]] == sum(m["lane_pages"])
+    if m["numa_policy"] == "gpu":
+        assert m["copy_pieces"][m["gpu_numa_node"]] == sum(m["copy_pieces"])
+
+
+def test_pageable_image_registered_batch_by_batch_at_every_alignment(bt, oracle):
+    """The registered feed locks the whole pages of each batch and sends the
+    unaligned head / tail bytes through a small pinned edge buffer: images
+    starting on a page, 1, 16 and 4095 bytes past one, with a short last
+    chunk, hash exactly; no page stays registered after the call (the caller
+    can register the image itself afterwards)."""
+    import numpy as np
+    n = 140 * CHUNK + 12345
+    raw = np.frombuffer(bytes(oracle.fill_synthetic(n + 3 * 4096, 9, 0xA11C)), dtype=np.uint8).copy()
+    base = raw.ctypes.data
+    first_page = (-base) % 4096
+    for shift in (first_page, first_page + 1, first_page + 16, first_page + 4095):
+        addr = base + shift
+        want = b"".join(oracle.hash_chunks(bytes(raw[shift:shift + n]), CHUNK))
+        assert bt.chunks_host_addr(addr, n) == want, shift
+        s = bt.pipeline_stats()
+        assert (s["feed"], s["registered_batches"], s["chunks"]) == ("registered", 2, 141), shift
+        bt.host_register(addr, n)
+        bt.host_unregister(addr)
+
+
+def test_registered_feed_falls_back_to_staging_pages_it_cannot_lock(bt, oracle, tmp_path):
+    """Pages the registered feed cannot lock -- part of the image registered
+    by the caller already, or a read-only file mapping -- are staged through
+    the lane instead: exact digests either way, and the caller's own
+    registration is left as it was."""
+    import numpy as np
+    n = 150 * CHUNK
+    data = np.frombuffer(bytes(oracle.fill_synthetic(n, 21, 0xFA11)), dtype=np.uint8).copy()
+    want = b"".join(oracle.hash_chunks(bytes(data), CHUNK))
+    addr = data.ctypes.data
+    mid = addr + ((40 * CHUNK + 4095) & ~4095)
+    bt.host_register(mid, 8 * CHUNK)   # the caller's own registration inside batch 0
+    try:
+        assert bt.chunks_host_addr(addr, n) == want
+        assert bt.pipeline_stats()["feed"] == "registered"
+    finally:
+        bt.host_unregister(mid)        # still the caller's, still there
+    f = tmp_path / "ro.img"
+    f.write_bytes(data.tobytes())
+    ro = np.memmap(str(f), dtype=np.uint8, mode="r")
+    assert bt.chunks_host_addr(ro.ctypes.data, n) == want
+    del ro
+
+
+def test_pageable_stage_knob_keeps_the_staged_feed(tmp_path):
+    """BT_SHA1_PAGEABLE=stage: pageable input of any size is copied into the
+    staging lanes, as before round 6 (child process: the knob is read once)."""
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2]);"
+        "import btsha1 as bt, py_oracle as o;"
+        "d = np.frombuffer(bytes(o.fill_synthetic(130 * 524288 + 77, 3, 0x5EED)), dtype=np.uint8).copy();"
+        "w = b''.join(o.hash_chunks(bytes(d), 524288));"
+        "assert bt.chunks_host_addr(d.ctypes.data, d.nbytes) == w;"
+        "s = bt.pipeline_stats(); assert s['feed'] == 'staged' and sum(s['copy_pieces']) > 0, s;"
+        "print('ok', s['batches'])")
+    env = dict(os.environ, BT_SHA1_PAGEABLE="stage")
+    r = subprocess.run([sys.executable, "-c", code, PKG, os.path.join(REPO, "oracle")], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert r.returncode == 0 and "ok 2" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
 
 
 def test_registered_host_image_direct_dma(bt, oracle):

@@ -632,6 +632,7 @@ def timed_runs(fn, want, gib, steady=5, stats=None):
         if stats is not None:
             s = stats()
             row.update(fill_s=s["fill_s"], wait_s=s["wait_s"], alloc_s=s["alloc_s"], register_s=s["register_s"],
+                       unregister_s=s["unregister_s"],
                        fill_GiB_per_s=round(gib / s["fill_s"], 2) if s["fill_s"] > 0 else None)
         runs.append(row)
     steady_rates = [r["GiB_per_s"] for r in runs[1:]]
@@ -691,8 +692,8 @@ def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
         **timed_runs(lambda: bt.chunks_host_addr(addr, nbytes), want, gib, stats=bt.pipeline_stats),
         "numa": numa_view(bt.pipeline_stats()),
         "path": "bt_sha1_chunks_host on pageable memory (default feed): each ~1 GiB batch's whole pages "
-                "page-locked just ahead of its DMA and released after, unaligned edge bytes through a pinned "
-                "buffer, serial H2D on 2 streams, hot kernel, digests to pinned host"}
+                "page-locked just ahead of its DMA, all released after the last batch, unaligned edge bytes "
+                "through a pinned buffer, serial H2D on 2 streams, hot kernel, digests to pinned host"}
     # The same call with the pre-round-6 feed: 8 threads copy every byte into
     # page-locked staging lanes (on the GPU's NUMA node) ahead of the H2D --
     # its rate follows the host's free memory bandwidth and cores.

@@ -50,7 +50,7 @@ class PipelineStats(ctypes.Structure):  # include/bt_sha1.h bt_sha1_pipeline_sta
                 ("gpu_numa_node", ctypes.c_int32), ("numa_policy", ctypes.c_int32),
                 ("registered_batches", ctypes.c_int32),
                 ("total_s", ctypes.c_double), ("alloc_s", ctypes.c_double), ("fill_s", ctypes.c_double),
-                ("wait_s", ctypes.c_double), ("register_s", ctypes.c_double),
+                ("wait_s", ctypes.c_double), ("register_s", ctypes.c_double), ("unregister_s", ctypes.c_double),
                 ("lane_pages", ctypes.c_int32 * STATS_NODES), ("src_pages", ctypes.c_int32 * STATS_NODES),
                 ("copy_pieces", ctypes.c_int32 * STATS_NODES)]
 
@@ -338,7 +338,7 @@ def pipeline_stats():
     d = {k: getattr(s, k) for k, _ in PipelineStats._fields_}
     for k in ("lane_pages", "src_pages", "copy_pieces"):
         d[k] = list(d[k])[:nodes]
-    for k in ("total_s", "alloc_s", "fill_s", "wait_s", "register_s"):
+    for k in ("total_s", "alloc_s", "fill_s", "wait_s", "register_s", "unregister_s"):
         d[k] = round(d[k], 4)
     d["feed"] = {0: "direct", 1: "staged", 2: "registered"}.get(s.staged, "?")
     d["staged"], d["numa_policy"] = s.staged == 1, {1: "lanes", 2: "gpu"}.get(s.numa_policy, "none")

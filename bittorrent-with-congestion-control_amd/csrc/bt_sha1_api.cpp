@@ -354,7 +354,6 @@ struct Lane {
   DevBuf d_in;
   bool busy = false;
   uint64_t first = 0, count = 0;  // chunk range in flight
-  void *reg = nullptr;  // caller pages registered for the batch in flight (unregistered once it is done)
 };
 
 struct DevCtx {
@@ -633,8 +632,7 @@ int64_t parallel_pread(int fd, uint8_t *dst, uint64_t want, uint64_t pos) {
 // place when the DMA engine can read it) and returns the byte count -- fewer
 // than max_bytes at a piece boundary of its own -- setting eof when no input
 // follows (a return of 0 is the end too); sink(first_chunk, count, digests)
-// receives digests in chunk order.  A fill may register caller pages for the
-// batch (lane.reg): they are unregistered once the lane's batch is done.
+// receives digests in chunk order.
 // BT_SHA1_TRACE=1: per-phase wall times of each pipeline run on stderr.
 bool trace_on() {
   static const bool on = [] {
@@ -690,8 +688,8 @@ enum class Feed {
   kRegistered  // pageable caller memory page-locked batch by batch (chunks_host_on)
 };
 
-// Registration time of the calling thread's current pipeline run (the
-// registered feed's fill adds to it; drain adds the unregistration).
+// Registration of the calling thread's current pipeline run (the registered
+// feed's fill adds to it).
 thread_local double t_register = 0;
 thread_local uint32_t t_registered_batches = 0;
 
@@ -773,30 +771,11 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
     if (pre_rc) set_err("%s", pre_err.c_str());
     return pre_rc;
   };
-  // Caller pages a fill registered for a batch stay registered until that
-  // batch's copies are done -- on every exit path, errors included.
-  struct UnregisterAtExit {
-    DevCtx *c;
-    ~UnregisterAtExit() {
-      for (auto &l : c->lane)
-        if (l.reg) {
-          (void)hipStreamSynchronize(l.s);
-          (void)hipHostUnregister(l.reg);
-          l.reg = nullptr;
-        }
-    }
-  } unregister_at_exit{c};
   auto drain = [&](Lane &l) -> int {
     if (!l.busy) return 0;
     const double t0 = now_s();
     BT_CK(hipEventSynchronize(l.ev));
     t_wait += now_s() - t0;
-    if (l.reg) {
-      const double t1 = now_s();
-      BT_CK(hipHostUnregister(l.reg));
-      l.reg = nullptr;
-      t_register += now_s() - t1;
-    }
     sink(l.first, l.count, l.h_dig.as<uint8_t>());
     l.busy = false;
     return 0;
@@ -938,6 +917,23 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   // caller elsewhere) are staged through the lane instead.
   uint64_t b1 = 0, p0 = 0, p1 = 0;
   bool locked = false;
+  // Locked ranges stay locked until the whole call is done: hipHostUnregister
+  // waits for the device's outstanding work, so releasing a batch's pages
+  // while the next batch's copy and hash are in flight stalled the pipeline
+  // (40.5 GiB/s instead of 50.7 on 8 GiB, profiles/r06).  At the end nothing
+  // is in flight and each release is quick; on an error path the lanes'
+  // streams are drained first.
+  std::vector<void *> regs;
+  struct UnlockAtExit {
+    DevCtx *c;
+    std::vector<void *> &regs;
+    ~UnlockAtExit() {
+      if (regs.empty()) return;
+      for (auto &l : c->lane)
+        if (l.s) (void)hipStreamSynchronize(l.s);
+      for (void *p : regs) (void)hipHostUnregister(p);
+    }
+  } unlock_at_exit{c, regs};
   auto fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src, bool *eof) -> int64_t {
     uint64_t n = std::min<uint64_t>(max, total - off);
     if (feed == Feed::kDirect) {
@@ -957,7 +953,7 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
           const hipError_t e = hipHostRegister((void *)(h_in + p0), (size_t)(p1 - p0), hipHostRegisterPortable);
           t_register += now_s() - t0;
           if (e == hipSuccess) {
-            l.reg = (void *)(h_in + p0);
+            regs.push_back((void *)(h_in + p0));
             locked = true;
             ++t_registered_batches;
           } else {
@@ -997,6 +993,17 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   if (n >= 0 && t_stats_valid) {
     t_stats.bytes = total;
     page_nodes(h_in, total, 64, t_stats.src_pages, BT_SHA1_STATS_NODES);
+  }
+  if (n >= 0 && !regs.empty()) {  // every batch is done: release the pages (timed into the call's stats)
+    const double t0 = now_s();
+    for (void *p : regs)
+      if (hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
+    regs.clear();
+    const double dt = now_s() - t0;
+    if (t_stats_valid) {
+      t_stats.unregister_s = dt;
+      t_stats.total_s += dt;
+    }
   }
   return n;
 }

@@ -2,14 +2,14 @@
 (2 x <= 1 GiB, include/bt_sha1.h) is freed before it returns, for the
 default 1 GiB direct-DMA batches (kept, never freed) and for bigger ones
 (BT_SHA1_DMA_BATCH_MB=4096: grown for the call, then shrunk back to the kept
-lane), registered and pageable input, single worker and repeated device ids
+lane), registered and pageable input (page-locked batch by batch), single worker and repeated device ids
 (devs=[0,0,0]).  Both ways: no call holds more than the kept lanes after it
 returns, and no call frees the kept lanes either (the next staged call would
 pay for pinning them again).
 
 The batch size is read once per process, so each setting runs in a child
 process; hipMemGetInfo after each call is compared with the level after a
-first pageable call that sized the kept lanes, and every call's digests with
+first pageable call (staged feed) that sized the kept lanes, and every call's digests with
 the oracle on sampled chunks and with each other."""
 import json
 import os
@@ -37,7 +37,9 @@ def _child():
     words = img.view(np.uint64)
     words[:] = np.arange(words.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
     addr = img.ctypes.data
-    want = bt.chunks_host_addr(addr, img.nbytes)  # pageable: sizes the kept lanes
+    prev = bt.set_pageable_feed("stage")
+    want = bt.chunks_host_addr(addr, img.nbytes)  # pageable, staged: sizes the kept lanes
+    bt.set_pageable_feed(prev)
     ok = all(want[20 * i:20 * i + 20] == orc.sha1(img[i * CHUNK:(i + 1) * CHUNK].tobytes()) for i in (0, 4097, n - 1))
 
     def free_now():
@@ -45,6 +47,7 @@ def _child():
         return torch.cuda.mem_get_info()[0]
     kept = free_now()
     levels = {}
+    levels["pageable"] = (bt.chunks_host_addr(addr, img.nbytes) == want, free_now())  # page-locked batch by batch
     levels["pageable_devs3"] = (bt.chunks_host_addr(addr, img.nbytes, devs=[0, 0, 0]) == want, free_now())
     bt.host_register(addr, img.nbytes)
     try:

@@ -89,6 +89,45 @@ int main(int argc, char **argv) {
     free(b);
   }
 
+  /* pageable input >= 64 MiB: the registered feed (each batch's whole pages
+   * locked and DMA'd in place, the unaligned head / tail bytes through the
+   * lane's edge buffer) at random start alignments, totals and chunk sizes,
+   * against the staged feed over the same bytes */
+  {
+    const uint64_t big = 96ull << 20;
+    uint8_t *pool = malloc(big + 8192);
+    for (uint64_t o = 0; o < big + 8192; o += 4 * BT_CHUNK_SIZE) {
+      const uint64_t k = big + 8192 - o < 4 * BT_CHUNK_SIZE ? big + 8192 - o : 4 * BT_CHUNK_SIZE;
+      memcpy(pool + o, img, k);
+      pool[o] ^= (uint8_t)(o >> 20); /* no two 2 MiB tiles alike */
+    }
+    for (int t = 0; t < 4; t++) {
+      const uint64_t shift = rnd(8192), total = (64ull << 20) + rnd(32u << 20);
+      const uint64_t cl = t == 0 ? BT_CHUNK_SIZE : 4096 * (1 + rnd(200)) + rnd(4096);
+      const uint64_t n = (total + cl - 1) / cl;
+      uint8_t *a = malloc(20 * n), *b = malloc(20 * n);
+      CHECK(bt_sha1_chunks_host(pool + shift, total, cl, a) == (int64_t)n, "registered feed count: %s",
+            bt_sha1_last_error());
+      bt_sha1_pipeline_stats st;
+      CHECK(bt_sha1_get_pipeline_stats(&st) == 0 && st.staged == 2 && st.registered_batches == (int32_t)st.batches &&
+                st.chunks == n && st.bytes == total,
+            "registered feed stats (feed %d, %d of %u batches locked)", st.staged, st.registered_batches, st.batches);
+      CHECK(bt_sha1_set_pageable_feed(BT_SHA1_PAGEABLE_STAGE) == BT_SHA1_PAGEABLE_REGISTER, "feed switch");
+      CHECK(bt_sha1_chunks_host(pool + shift, total, cl, b) == (int64_t)n, "staged feed count");
+      CHECK(bt_sha1_get_pipeline_stats(&st) == 0 && st.staged == 1, "staged feed stats");
+      CHECK(bt_sha1_set_pageable_feed(BT_SHA1_PAGEABLE_REGISTER) == BT_SHA1_PAGEABLE_STAGE, "feed switch back");
+      CHECK(!memcmp(a, b, 20 * n), "registered vs staged feed (shift %llu, total %llu, chunk %llu)",
+            (unsigned long long)shift, (unsigned long long)total, (unsigned long long)cl);
+      uint8_t d[20];
+      shahash(pool + shift + (n - 1) * cl, (int)(total - (n - 1) * cl), d);
+      CHECK(!memcmp(d, a + 20 * (n - 1), 20), "registered feed short tail");
+      free(a);
+      free(b);
+    }
+    CHECK(bt_sha1_set_pageable_feed(7) == -1, "bad feed accepted");
+    free(pool);
+  }
+
   /* verifier ring: up to 6 outstanding slots, random commit / release order */
   bt_sha1_verifier *v = bt_sha1_verifier_create(0, BT_CHUNK_SIZE, 5, 4);
   CHECK(v != NULL, "verifier_create: %s", bt_sha1_last_error());

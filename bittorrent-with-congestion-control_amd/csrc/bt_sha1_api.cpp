@@ -19,7 +19,6 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
-#include <condition_variable>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -689,6 +688,11 @@ enum class Feed {
   kRegistered  // pageable caller memory page-locked batch by batch (chunks_host_on)
 };
 
+// Registration of the calling thread's current pipeline run (the registered
+// feed's fill adds to it).
+thread_local double t_register = 0;
+thread_local uint32_t t_registered_batches = 0;
+
 template <class Fill, class Sink>
 int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed feed, Fill fill, Sink sink) {
   if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
@@ -698,6 +702,8 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
   const bool staged = feed == Feed::kStaged;
   const double t_start = now_s();
   double t_fill = 0, t_wait = 0;
+  t_register = 0;
+  t_registered_batches = 0;
   if (ensure_streams(c)) return -1;
   const uint64_t bytes_per = batch_bytes_for(chunk_len, size_hint, staged);
   const uint64_t per = bytes_per / chunk_len;
@@ -839,6 +845,8 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
   s.batch_bytes = bytes_per;
   s.batches = (uint32_t)k;
   s.staged = feed == Feed::kStaged ? 1 : feed == Feed::kRegistered ? 2 : 0;
+  s.registered_batches = (int32_t)t_registered_batches;
+  s.register_s = t_register;
   s.device = c->dev;
   s.copy_threads = copy_threads();
   s.numa_nodes = numa_topo().nodes;
@@ -884,86 +892,6 @@ int pageable_feed() {
 }
 bool register_pageable() { return pageable_feed() == BT_SHA1_PAGEABLE_REGISTER; }
 
-// Locks the whole pages of each batch of a pageable image, in batch order,
-// on a thread of its own (registered feed of chunks_host_on).
-struct PageLocker {
-  const uint8_t *base;
-  uint64_t total, batch;
-  std::vector<uint64_t> p0, p1;  // per batch: its whole pages [p0, p1) (offsets into the image)
-  std::vector<int8_t> state;     // per batch: 0 pending, 1 locked, 2 not locked (staged)
-  std::mutex mu;
-  std::condition_variable cv;
-  size_t done = 0;      // batches decided
-  bool finished = false;
-  std::atomic<bool> stop{false};
-  double lock_s = 0;    // time spent locking (the helper's)
-  std::thread th;
-
-  PageLocker(const uint8_t *b, uint64_t t, uint64_t bt) : base(b), total(t), batch(bt) {
-    const size_t nb = t ? (size_t)((t + bt - 1) / bt) : 0;
-    p0.resize(nb);
-    p1.resize(nb);
-    state.assign(nb, 0);
-    const uintptr_t a = (uintptr_t)b;
-    for (size_t k = 0; k < nb; ++k) {
-      const uint64_t lo = k * bt, hi = std::min<uint64_t>(lo + bt, t);
-      p0[k] = ((a + lo + kPage - 1) & ~(uintptr_t)(kPage - 1)) - a;
-      p1[k] = ((a + hi) & ~(uintptr_t)(kPage - 1)) - a;
-      if (p1[k] <= p0[k]) p0[k] = p1[k] = hi;  // no whole page: the batch (< 2 pages) rides in the edge buffer
-    }
-  }
-  void start(int dev) {
-    th = std::thread([this, dev] {
-      (void)hipSetDevice(dev);
-      for (size_t k = 0; k < state.size() && !stop.load(); ++k) {
-        int8_t st = 2;
-        if (p1[k] > p0[k]) {
-          const double t0 = now_s();
-          const hipError_t e = hipHostRegister((void *)(base + p0[k]), (size_t)(p1[k] - p0[k]), hipHostRegisterPortable);
-          lock_s += now_s() - t0;
-          if (e == hipSuccess) st = 1;
-          else (void)hipGetLastError();  // that batch is staged
-        }
-        std::lock_guard<std::mutex> g(mu);
-        state[k] = st;
-        done = k + 1;
-        cv.notify_all();
-      }
-      std::lock_guard<std::mutex> g(mu);
-      finished = true;
-      cv.notify_all();
-    });
-  }
-  // true when batch k's pages are locked (waits for the helper to get there)
-  bool wait(size_t k) {
-    std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return done > k || finished; });
-    return k < state.size() && state[k] == 1;
-  }
-  void stop_and_join() {
-    stop.store(true);
-    if (th.joinable()) th.join();
-  }
-  bool any_locked() const {
-    for (int8_t s : state)
-      if (s == 1) return true;
-    return false;
-  }
-  int32_t locked_count() const {
-    int32_t n = 0;
-    for (int8_t s : state) n += s == 1;
-    return n;
-  }
-  void unlock_all() {  // after stop_and_join, with nothing in flight
-    for (size_t k = 0; k < state.size(); ++k)
-      if (state[k] == 1) {
-        if (hipHostUnregister((void *)(base + p0[k])) != hipSuccess) (void)hipGetLastError();
-        state[k] = 2;
-      }
-  }
-  ~PageLocker() { stop_and_join(); }
-};
-
 // own: a worker context of this call (repeated device ids); NULL = the
 // device's shared context.
 int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t chunk_len, uint8_t *h_dig,
@@ -982,36 +910,30 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
                                                                       : Feed::kStaged;
   uint64_t off = 0;
   // Registered feed, per batch [b0, b1) of the input: the whole pages inside
-  // it, [p0, p1), are page-locked and DMA'd in place; the head [b0, p0) and
-  // tail [p1, b1) -- under a page each, shared with the neighbouring batch's
-  // pages -- go through the lane's small pinned edge buffer.  Pages that
-  // cannot be registered (read-only, registered by the caller elsewhere) are
-  // staged through the lane instead.  A helper thread locks the batches in
-  // order ahead of the pipeline (first-time locking costs ~10 ms per GiB
-  // against ~19 ms for the batch's DMA; pages locked before, ~0.1 ms), and
-  // the fill of batch k waits only for batch k's lock.
-  const uint64_t batch = batch_bytes_for(chunk_len, total, false);
-  PageLocker locker(h_in, feed == Feed::kRegistered ? total : 0, batch);
+  // it, [p0, p1), are page-locked for the batch and DMA'd in place; the head
+  // [b0, p0) and tail [p1, b1) -- under a page each, shared with the
+  // neighbouring batch's pages -- go through the lane's small pinned edge
+  // buffer.  Pages that cannot be registered (read-only, registered by the
+  // caller elsewhere) are staged through the lane instead.
+  uint64_t b1 = 0, p0 = 0, p1 = 0;
+  bool locked = false;
   // Locked ranges stay locked until the whole call is done: hipHostUnregister
   // waits for the device's outstanding work, so releasing a batch's pages
   // while the next batch's copy and hash are in flight stalled the pipeline
   // (40.5 GiB/s instead of 50.7 on 8 GiB, profiles/r06).  At the end nothing
   // is in flight and each release is quick; on an error path the lanes'
   // streams are drained first.
+  std::vector<void *> regs;
   struct UnlockAtExit {
     DevCtx *c;
-    PageLocker &locker;
+    std::vector<void *> &regs;
     ~UnlockAtExit() {
-      locker.stop_and_join();
-      if (!locker.any_locked()) return;
+      if (regs.empty()) return;
       for (auto &l : c->lane)
         if (l.s) (void)hipStreamSynchronize(l.s);
-      locker.unlock_all();
+      for (void *p : regs) (void)hipHostUnregister(p);
     }
-  } unlock_at_exit{c, locker};
-  if (feed == Feed::kRegistered) locker.start(dev);
-  uint64_t b1 = 0, p0 = 0, p1 = 0;
-  bool locked = false;
+  } unlock_at_exit{c, regs};
   auto fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src, bool *eof) -> int64_t {
     uint64_t n = std::min<uint64_t>(max, total - off);
     if (feed == Feed::kDirect) {
@@ -1020,12 +942,26 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
       parallel_copy(l.h_in.as<uint8_t>() + at, h_in + off, n);
       *src = l.h_in.as<uint8_t>() + at;
     } else {
-      if (at == 0) {  // a new batch: its pages' lock (taken by the helper)
-        const uint64_t k = off / batch;
-        locked = locker.wait(k);
-        p0 = locker.p0[k];
-        p1 = locker.p1[k];
-        b1 = std::min<uint64_t>((k + 1) * batch, total);
+      if (at == 0) {  // a new batch: lock its whole pages
+        b1 = off + n;
+        const uintptr_t base = (uintptr_t)h_in;
+        p0 = ((base + off + kPage - 1) & ~(uintptr_t)(kPage - 1)) - base;
+        p1 = ((base + b1) & ~(uintptr_t)(kPage - 1)) - base;
+        locked = false;
+        if (p1 > p0) {
+          const double t0 = now_s();
+          const hipError_t e = hipHostRegister((void *)(h_in + p0), (size_t)(p1 - p0), hipHostRegisterPortable);
+          t_register += now_s() - t0;
+          if (e == hipSuccess) {
+            regs.push_back((void *)(h_in + p0));
+            locked = true;
+            ++t_registered_batches;
+          } else {
+            (void)hipGetLastError();  // staged below
+          }
+        } else {
+          p0 = p1 = b1;  // no whole page: the batch (< 2 pages) rides in the edge buffer
+        }
       }
       uint8_t *edge = l.h_edge.as<uint8_t>();
       if (off < p0) {  // head, or a batch without a whole page
@@ -1058,14 +994,13 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
     t_stats.bytes = total;
     page_nodes(h_in, total, 64, t_stats.src_pages, BT_SHA1_STATS_NODES);
   }
-  if (n >= 0 && feed == Feed::kRegistered) {  // every batch is done: release the pages (timed into the stats)
-    locker.stop_and_join();
+  if (n >= 0 && !regs.empty()) {  // every batch is done: release the pages (timed into the call's stats)
     const double t0 = now_s();
-    locker.unlock_all();
+    for (void *p : regs)
+      if (hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
+    regs.clear();
     const double dt = now_s() - t0;
     if (t_stats_valid) {
-      t_stats.register_s = locker.lock_s;
-      t_stats.registered_batches = locker.locked_count();
       t_stats.unregister_s = dt;
       t_stats.total_s += dt;
     }

@@ -688,11 +688,6 @@ enum class Feed {
   kRegistered  // pageable caller memory page-locked batch by batch (chunks_host_on)
 };
 
-// Registration of the calling thread's current pipeline run (the registered
-// feed's fill adds to it).
-thread_local double t_register = 0;
-thread_local uint32_t t_registered_batches = 0;
-
 template <class Fill, class Sink>
 int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed feed, Fill fill, Sink sink) {
   if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
@@ -702,8 +697,6 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
   const bool staged = feed == Feed::kStaged;
   const double t_start = now_s();
   double t_fill = 0, t_wait = 0;
-  t_register = 0;
-  t_registered_batches = 0;
   if (ensure_streams(c)) return -1;
   const uint64_t bytes_per = batch_bytes_for(chunk_len, size_hint, staged);
   const uint64_t per = bytes_per / chunk_len;
@@ -845,8 +838,6 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
   s.batch_bytes = bytes_per;
   s.batches = (uint32_t)k;
   s.staged = feed == Feed::kStaged ? 1 : feed == Feed::kRegistered ? 2 : 0;
-  s.registered_batches = (int32_t)t_registered_batches;
-  s.register_s = t_register;
   s.device = c->dev;
   s.copy_threads = copy_threads();
   s.numa_nodes = numa_topo().nodes;
@@ -910,13 +901,19 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
                                                                       : Feed::kStaged;
   uint64_t off = 0;
   // Registered feed, per batch [b0, b1) of the input: the whole pages inside
-  // it, [p0, p1), are page-locked for the batch and DMA'd in place; the head
-  // [b0, p0) and tail [p1, b1) -- under a page each, shared with the
-  // neighbouring batch's pages -- go through the lane's small pinned edge
-  // buffer.  Pages that cannot be registered (read-only, registered by the
-  // caller elsewhere) are staged through the lane instead.
-  uint64_t b1 = 0, p0 = 0, p1 = 0;
-  bool locked = false;
+  // it, [p0, p1), are page-locked and DMA'd in place; the head [b0, p0) and
+  // tail [p1, b1) -- under a page each, shared with the neighbouring batch's
+  // pages -- go through the lane's small pinned edge buffer.  Pages that
+  // cannot be registered (read-only, registered by the caller elsewhere) are
+  // staged through the lane instead.  Every batch is locked before the first
+  // copy is queued: locking pages never locked before takes ~2 ms per GiB
+  // with the device idle, but waits for the device when copies are in flight
+  // -- locking each batch just ahead of its DMA cost the first call 78-86 ms
+  // per 8 GiB (31-36 GiB/s; profiles/r06).
+  const uint64_t batch = batch_bytes_for(chunk_len, total, false);
+  const size_t nbatch = feed == Feed::kRegistered ? (size_t)((total + batch - 1) / batch) : 0;
+  std::vector<uint64_t> bp0(nbatch), bp1(nbatch);
+  std::vector<char> blocked(nbatch, 0);
   // Locked ranges stay locked until the whole call is done: hipHostUnregister
   // waits for the device's outstanding work, so releasing a batch's pages
   // while the next batch's copy and hash are in flight stalled the pipeline
@@ -934,6 +931,29 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
       for (void *p : regs) (void)hipHostUnregister(p);
     }
   } unlock_at_exit{c, regs};
+  double lock_s = 0;
+  if (nbatch) {
+    const double t0 = now_s();
+    const uintptr_t base = (uintptr_t)h_in;
+    for (size_t k = 0; k < nbatch; ++k) {
+      const uint64_t lo = k * batch, hi = std::min<uint64_t>(lo + batch, total);
+      bp0[k] = ((base + lo + kPage - 1) & ~(uintptr_t)(kPage - 1)) - base;
+      bp1[k] = ((base + hi) & ~(uintptr_t)(kPage - 1)) - base;
+      if (bp1[k] <= bp0[k]) {
+        bp0[k] = bp1[k] = hi;  // no whole page: the batch (< 2 pages) rides in the edge buffer
+        continue;
+      }
+      if (hipHostRegister((void *)(h_in + bp0[k]), (size_t)(bp1[k] - bp0[k]), hipHostRegisterPortable) == hipSuccess) {
+        regs.push_back((void *)(h_in + bp0[k]));
+        blocked[k] = 1;
+      } else {
+        (void)hipGetLastError();  // that batch is staged
+      }
+    }
+    lock_s = now_s() - t0;
+  }
+  uint64_t b1 = 0, p0 = 0, p1 = 0;
+  bool locked = false;
   auto fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src, bool *eof) -> int64_t {
     uint64_t n = std::min<uint64_t>(max, total - off);
     if (feed == Feed::kDirect) {
@@ -942,26 +962,12 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
       parallel_copy(l.h_in.as<uint8_t>() + at, h_in + off, n);
       *src = l.h_in.as<uint8_t>() + at;
     } else {
-      if (at == 0) {  // a new batch: lock its whole pages
-        b1 = off + n;
-        const uintptr_t base = (uintptr_t)h_in;
-        p0 = ((base + off + kPage - 1) & ~(uintptr_t)(kPage - 1)) - base;
-        p1 = ((base + b1) & ~(uintptr_t)(kPage - 1)) - base;
-        locked = false;
-        if (p1 > p0) {
-          const double t0 = now_s();
-          const hipError_t e = hipHostRegister((void *)(h_in + p0), (size_t)(p1 - p0), hipHostRegisterPortable);
-          t_register += now_s() - t0;
-          if (e == hipSuccess) {
-            regs.push_back((void *)(h_in + p0));
-            locked = true;
-            ++t_registered_batches;
-          } else {
-            (void)hipGetLastError();  // staged below
-          }
-        } else {
-          p0 = p1 = b1;  // no whole page: the batch (< 2 pages) rides in the edge buffer
-        }
+      if (at == 0) {  // a new batch
+        const size_t k = (size_t)(off / batch);
+        p0 = bp0[k];
+        p1 = bp1[k];
+        b1 = std::min<uint64_t>((k + 1) * batch, total);
+        locked = blocked[k] != 0;
       }
       uint8_t *edge = l.h_edge.as<uint8_t>();
       if (off < p0) {  // head, or a batch without a whole page
@@ -994,16 +1000,18 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
     t_stats.bytes = total;
     page_nodes(h_in, total, 64, t_stats.src_pages, BT_SHA1_STATS_NODES);
   }
-  if (n >= 0 && !regs.empty()) {  // every batch is done: release the pages (timed into the call's stats)
+  if (n >= 0 && feed == Feed::kRegistered) {  // every batch is done: release the pages (timed into the stats)
     const double t0 = now_s();
     for (void *p : regs)
       if (hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
-    regs.clear();
     const double dt = now_s() - t0;
     if (t_stats_valid) {
+      t_stats.registered_batches = (int32_t)regs.size();
+      t_stats.register_s = lock_s;
       t_stats.unregister_s = dt;
-      t_stats.total_s += dt;
+      t_stats.total_s += lock_s + dt;
     }
+    regs.clear();
   }
   return n;
 }

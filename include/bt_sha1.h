@@ -192,8 +192,9 @@ int64_t bt_sha1_chunks_file(void *fp /* FILE* */, uint64_t chunk_len, uint8_t *h
  * within the caller's affinity mask -- measured 15-30 % slower on a shared
  * host, where the node's cores are busy with other work: DESIGN.md §6).
  * Pageable input of at least 64 MiB to bt_sha1_chunks_host is page-locked
- * batch by batch (the whole pages of each ~1 GiB batch, just before its DMA;
- * all released when the call's last batch is done) and DMA'd in place; the unaligned head
+ * batch by batch (the whole pages of each ~1 GiB batch, all locked before the
+ * first copy and released when the call's last batch is done) and DMA'd in
+ * place; the unaligned head
  * and tail bytes of each batch, and pages that cannot be locked, are staged
  * (BT_SHA1_PAGEABLE=stage: stage everything).
  * Returns 0, or -1 when this thread has run no pipeline. */
@@ -224,7 +225,8 @@ typedef struct {
   double fill_s;            /* providing the input on the host: staging copies
                                / reads, or registering the batch's pages      */
   double wait_s;            /* blocked on a lane's H2D + hash                 */
-  double register_s;        /* page-locking caller pages (inside fill_s)      */
+  double register_s;        /* page-locking caller pages before the first copy
+                               (in total_s)                                   */
   double unregister_s;      /* releasing them after the last batch (in total_s) */
   int32_t lane_pages[BT_SHA1_STATS_NODES];  /* sampled staging pages per node */
   int32_t src_pages[BT_SHA1_STATS_NODES];   /* sampled input pages per node   */

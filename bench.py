@@ -305,9 +305,8 @@ class DeviceHasher:
                 "pairs": pairs,
                 "flags_correct": bool(torch.equal(ok, want)), "mismatches_planted": int(bad.numel()),
                 "kernel": self.bt.kernel_name(self.C),
-                "path": "bt_sha1_verify_dev: the hot kernel with its fused compare epilogue (util.c:311-313) "
-                        "against expected digests in HBM, paired with bt_sha1_chunks_dev in one window (ABBA "
-                        "order, per-launch HIP events on the hasher's stream), one untimed launch of each first"}
+                "path": "bt_sha1_verify_dev (fused compare, util.c:311-313) vs bt_sha1_chunks_dev: ABBA pairs "
+                        "in one window, per-launch HIP events, one untimed launch of each first"}
 
     def clock_mhz(self, launches=3):
         """Median in-kernel shader clock over the waves of the last of
@@ -458,10 +457,8 @@ def _power_window(smi, h, hasher, seconds):
         "limiter_residency": residency,
         "temperature_C": {k: m1.get(f"temperature_{k}") for k in ("hotspot", "mem")},
         "launches": n, "window_s": round(t1 - t0, 3), "samples": len(samples),
-        "method": "after the timed region: the timed step launched back to back; socket_W = SMU energy "
-                  "accumulator delta / wall time (amdsmi_get_energy_count); samples = gpu_metrics "
-                  "current_socket_power / current_gfxclks every 50 ms, median of the second half; "
-                  "limiter_residency = fraction of SMU ticks each limiter (ppt = package power) was active",
+        "method": "timed step back to back after the timed region; socket_W = SMU energy accumulator delta / "
+                  "wall; samples every 50 ms (median of the 2nd half); limiter_residency = fraction of SMU ticks",
     }
 
 
@@ -570,10 +567,9 @@ def cpu_baseline(host_addr, n_chunks, gpu_digests, min_s=1.0, reps=3):
     per_core = rows.get("O2_1t", {}).get("GiB_per_s")
     return {
         "value": head["GiB_per_s"], "unit": "GiB/s", "cores": cores, "threads": head["threads"], "kind": kind,
-        "sample": f"{n_chunks} x 512 KiB chunks ({n_chunks * CHUNK / 2**30:.1f} GiB) of the benchmark's own "
-                  f"synthetic chunks ({n1} on 1 thread), shahash per chunk (chunk.c:21), static split; each "
-                  f"rate = median of {reps} measurements of >= {min_s:g} s; value = the best -O2 rate with "
-                  f"`cores` (= min(affinity {affinity}, ceil(cgroup quota {quota}))) or {affinity} threads",
+        "sample": f"{n_chunks} x 512 KiB of the bench's chunks ({n1} on 1 thread), shahash per chunk (chunk.c:21); "
+                  f"rate = median of {reps} runs of >= {min_s:g} s; value = best -O2 multi-thread run; cores = "
+                  f"min(affinity {affinity}, ceil(quota {quota}))",
         "flags": head["flags"], "digests_match_gpu": all(r["digests_match_gpu"] for r in rows.values()),
         "per_core_GiB_per_s_O2": per_core,
         "quota_bound_GiB_per_s": round(per_core * quota, 3) if per_core and quota else None,
@@ -609,12 +605,12 @@ def machine_cpu_ticks():
 
 
 def timed_runs(fn, want, gib, steady=5, stats=None):
-    """The first run of a host path (it also pays one-time pinning), then
-    `steady` more; value = the MEDIAN steady run.  Every run is listed with
-    its wall time, the CPU time this process spent in it, the time the
-    cgroup's quota throttled it and -- with stats (bt.pipeline_stats) -- the
-    pipeline's own phase split: host staging (fill), blocked on the GPU lane
-    (wait), allocation (alloc)."""
+    """The first run of a host path (it also pays one-time pinning / page
+    locking), then `steady` more; value = the MEDIAN steady run.  Every run's
+    rate is listed; the median run and the first run carry their breakdown
+    (HOST_PATH_FIELDS): wall time, this process's CPU time, the time the
+    cgroup's quota throttled it, the whole machine's CPU busy fraction and --
+    with stats (bt.pipeline_stats) -- the pipeline's own phase split."""
     import statistics
     runs, ok = [], True
     for _ in range(1 + steady):
@@ -626,40 +622,41 @@ def timed_runs(fn, want, gib, steady=5, stats=None):
         ok = ok and r == want
         row = {"GiB_per_s": round(gib / dt, 3), "s": round(dt, 4), "cpu_s": round(cpu, 3)}
         if cg0 and cg1:
-            row["cgroup_throttled_s"] = round(cg1["throttled_s"] - cg0["throttled_s"], 4)
+            row["throttled_s"] = round(cg1["throttled_s"] - cg0["throttled_s"], 4)
         if m0 and m1 and m1[1] > m0[1]:
-            row["machine_cpu_busy"] = round((m1[0] - m0[0]) / (m1[1] - m0[1]), 3)
+            row["host_busy"] = round((m1[0] - m0[0]) / (m1[1] - m0[1]), 3)
         if stats is not None:
-            s = stats()
-            row.update(fill_s=s["fill_s"], wait_s=s["wait_s"], alloc_s=s["alloc_s"], register_s=s["register_s"],
-                       unregister_s=s["unregister_s"],
-                       fill_GiB_per_s=round(gib / s["fill_s"], 2) if s["fill_s"] > 0 else None)
+            st = stats()
+            row.update(fill_s=st["fill_s"], wait_s=st["wait_s"], alloc_s=st["alloc_s"], lock_s=st["register_s"],
+                       unlock_s=st["unregister_s"])
         runs.append(row)
     steady_rates = [r["GiB_per_s"] for r in runs[1:]]
-    med = statistics.median(steady_rates)
-    out = {"GiB_per_s": round(med, 3), "first_run_GiB_per_s": runs[0]["GiB_per_s"],
-           "steady_min_max": [min(steady_rates), max(steady_rates)], "digests_match": ok,
-           "statistic": f"median of {steady} steady-state runs after the first", "runs": runs}
-    if stats is not None:
-        mid = sorted(runs[1:], key=lambda r: r["GiB_per_s"])[len(runs[1:]) // 2]
-        out["median_run_phases"] = {k: mid[k] for k in ("s", "fill_s", "wait_s", "alloc_s")}
-        out["median_run_phases"]["fill_frac"] = round(mid["fill_s"] / mid["s"], 3) if mid["s"] > 0 else None
+    mid = sorted(runs[1:], key=lambda r: r["GiB_per_s"])[len(runs[1:]) // 2]
+    out = {"GiB_per_s": round(statistics.median(steady_rates), 3), "first_run_GiB_per_s": runs[0]["GiB_per_s"],
+           "runs_GiB_per_s": [r["GiB_per_s"] for r in runs], "digests_match": ok,
+           "median_run": {k: v for k, v in mid.items() if k != "GiB_per_s"},
+           "first_run": {k: v for k, v in runs[0].items() if k in ("s", "alloc_s", "lock_s", "fill_s", "wait_s")}}
+    if stats is not None and mid["s"] > 0:
+        out["median_run"]["fill_frac"] = round(mid["fill_s"] / mid["s"], 3)
     return out
+
+
+HOST_PATH_FIELDS = (
+    "GiB_per_s = median of runs 2-6 (runs_GiB_per_s: all 6); median_run / first_run: s wall, cpu_s process CPU, "
+    "throttled_s cgroup throttling, host_busy whole-machine CPU busy, fill_s host-side input (copies), wait_s "
+    "blocked on the GPU lane, lock_s / unlock_s page locking, fill_frac = fill_s / s; numa: feed, locked/all "
+    "batches, GPU node, image / lane pages and staging pieces per node, placement")
 
 
 def numa_view(st):
     """How a pipeline run was fed and where its memory sat, from
-    bt_sha1_get_pipeline_stats."""
-    return {"feed": st["feed"], "registered_batches": st["registered_batches"], "batches": st["batches"],
-            "numa_nodes": st["numa_nodes"], "gpu_node": st["gpu_numa_node"], "policy": st["numa_policy"],
-            "image_pages_per_node": st["src_pages"], "lane_pages_per_node": st["lane_pages"],
-            "staging_pieces_per_cpu_node": st["copy_pieces"], "copy_threads": st["copy_threads"],
-            "method": "move_pages() over 64 sampled pages of the image / of each staging lane; staging pieces "
-                      "counted by the node of the CPU their thread started on; the GPU's node from "
-                      "/sys/bus/pci/devices/<bdf>/numa_node"}
+    bt_sha1_get_pipeline_stats (fields in HOST_PATH_FIELDS)."""
+    return {"feed": st["feed"], "locked_batches": [st["registered_batches"], st["batches"]],
+            "gpu_node": st["gpu_numa_node"], "image_pages": st["src_pages"], "lane_pages": st["lane_pages"],
+            "staging_pieces": st["copy_pieces"], "policy": st["numa_policy"], "copy_threads": st["copy_threads"]}
 
 
-def run_verify_stream(vs, args, n, label, timeout=300):
+def run_verify_stream(vs, args, timeout=300):
     """One bin/verify-stream run; its JSON summary beside the digests check."""
     r = subprocess.run([vs, *args], capture_output=True, text=True, timeout=timeout)
     lines = r.stdout.strip().splitlines()
@@ -669,9 +666,8 @@ def run_verify_stream(vs, args, n, label, timeout=300):
         res = {}
     row = {"GiB_per_s": res.get("GiB_per_s"),
            "digests_match": r.returncode == 0 and res.get("failed") == 0 and res.get("ok") == res.get("chunks"),
-           "chunks_verified": res.get("chunks"), "timed_chunks": res.get("timed_chunks"),
-           "receive_threads": res.get("receive_threads"), "verifiers": res.get("verifiers"),
-           "path": f"bin/verify-stream {' '.join(args[:-2])}: {n} received chunks, {label}"}
+           "chunks": res.get("chunks"), "timed_chunks": res.get("timed_chunks"),
+           "receive_threads": res.get("receive_threads"), "args": " ".join(args[:-2])}
     if res.get("late_fills"):
         row["late_fills"] = res["late_fills"]
     if r.returncode != 0:
@@ -682,38 +678,36 @@ def run_verify_stream(vs, args, n, label, timeout=300):
 def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
     """host: pageable numpy image of the first chunks of dev_buf; want: their
     device-resident digests.  Each pipeline rate is the median of 5
-    steady-state runs after a first run (which also pays the one-time pinned
-    staging allocation), every run listed with its phase split."""
+    steady-state runs after a first one (which also pays one-time pinning /
+    page locking); the fields are described in the line itself (`fields`)."""
     addr, nbytes = host.ctypes.data, host.nbytes
     gib = nbytes / 2**30
-    out = {"image_GiB": round(gib, 3)}
+    out = {"image_GiB": round(gib, 3), "fields": HOST_PATH_FIELDS}
 
+    # Pageable image, default feed: each ~1 GiB batch's whole pages page-locked
+    # (all before the first copy, released after the last batch), DMA'd in
+    # place, unaligned edge bytes through a pinned buffer.
     out["pageable_chunks_host"] = {
         **timed_runs(lambda: bt.chunks_host_addr(addr, nbytes), want, gib, stats=bt.pipeline_stats),
-        "numa": numa_view(bt.pipeline_stats()),
-        "path": "bt_sha1_chunks_host on pageable memory (default feed): each ~1 GiB batch's whole pages "
-                "page-locked just ahead of its DMA, all released after the last batch, unaligned edge bytes "
-                "through a pinned buffer, serial H2D on 2 streams, hot kernel, digests to pinned host"}
-    # The same call with the pre-round-6 feed: 8 threads copy every byte into
-    # page-locked staging lanes (on the GPU's NUMA node) ahead of the H2D --
-    # its rate follows the host's free memory bandwidth and cores.
+        "numa": numa_view(bt.pipeline_stats())}
+    # The same call with the staged feed: 8 threads copy every byte into
+    # page-locked lanes (on the GPU's NUMA node) ahead of the H2D -- its rate
+    # follows the host's spare memory bandwidth and cores.
     prev = bt.set_pageable_feed("stage")
     try:
         out["pageable_staged_copy"] = {
             **timed_runs(lambda: bt.chunks_host_addr(addr, nbytes), want, gib, stats=bt.pipeline_stats),
-            "numa": numa_view(bt.pipeline_stats()),
-            "path": "bt_sha1_chunks_host on pageable memory, BT_SHA1_PAGEABLE=stage: threaded staging memcpy "
-                    "into pinned lanes on the GPU's NUMA node, 2-stream H2D, hot kernel"}
+            "numa": numa_view(bt.pipeline_stats())}
     finally:
         bt.set_pageable_feed(prev)
     t0 = time.perf_counter()
     bt.host_register(addr, nbytes)
     reg_s = time.perf_counter() - t0
     try:
+        # the caller registered the whole image: DMA straight from it
         out["registered_direct_dma"] = {
             **timed_runs(lambda: bt.chunks_host_addr(addr, nbytes), want, gib, stats=bt.pipeline_stats),
-            "register_s": round(reg_s, 3),
-            "path": "bt_sha1_host_register'ed image, H2D straight from it, 2 streams"}
+            "register_s": round(reg_s, 3)}
         pin = torch.from_numpy(host)
         scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev_buf.device)
         rates = []
@@ -724,18 +718,18 @@ def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
             torch.cuda.synchronize()
             rates.append(round(gib / (time.perf_counter() - t0), 3))
         del scratch
-        out["raw_h2d_ceiling"] = {"GiB_per_s": max(rates), "runs": rates,
-                                  "path": "one hipMemcpy of the registered image (best of 3)"}
+        out["raw_h2d_ceiling"] = {"GiB_per_s": max(rates), "runs": rates}  # one hipMemcpy of the registered image
     finally:
         bt.host_unregister(addr)
     for key in ("pageable_chunks_host", "pageable_staged_copy", "registered_direct_dma"):
         out[key]["frac_of_raw_h2d"] = round(out[key]["GiB_per_s"] / out["raw_h2d_ceiling"]["GiB_per_s"], 4)
     # The batched verifier (util.c:304-337 replacement): the product's C host
     # tool over a 1 GiB image in a tmpfs file.  Zero-copy: the receive landed
-    # the bytes in the pinned slots once, the timed rounds re-verify them (the
-    # H2D + hash + verdict bound).  Packetized: every timed round receives
+    # the bytes in the pinned slots once, the 8 timed rounds re-verify them
+    # (the H2D + hash + verdict bound).  Packetized: every timed round receives
     # each chunk again as util.c:275 does -- 1484-byte memcpys into the slot --
-    # on one receive thread, and on four (four verifiers, -g 4 -t).
+    # on one receive thread, and on four (four verifiers, -g 4 -t); 2 rounds
+    # timed after 1 untimed.
     vs = os.path.join(PKG, "bin", "verify-stream")
     n = min(int(verify_gib * 2**30) // CHUNK, nbytes // CHUNK)
     import shutil
@@ -748,17 +742,10 @@ def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
         with open(lst, "w") as f:
             for i in range(n):
                 f.write(f"{i} {want[20 * i:20 * i + 20].hex()}\n")
-        out["zero_copy_verifier"] = run_verify_stream(
-            vs, ["-z", "-b", "1024", "-s", "2", "-r", "9", img, lst], n,
-            "in pinned verifier slots, 8 steady-state rounds timed (H2D + hash + fused memcmp + verdicts)")
-        out["packetized_verifier"] = run_verify_stream(
-            vs, ["-b", "1024", "-s", "2", "-r", "3", "-w", "1", img, lst], n,
-            "each received again in every timed round as util.c:275 does (1484-byte memcpys into a pinned "
-            "slot), one receive thread, 2 rounds timed after 1 untimed")
+        out["zero_copy_verifier"] = run_verify_stream(vs, ["-z", "-b", "1024", "-s", "2", "-r", "9", img, lst])
+        out["packetized_verifier"] = run_verify_stream(vs, ["-b", "1024", "-s", "2", "-r", "3", "-w", "1", img, lst])
         out["packetized_verifier_4_threads"] = run_verify_stream(
-            vs, ["-g", "4", "-t", "-b", "256", "-s", "2", "-r", "3", "-w", "1", img, lst], n,
-            "1484-byte memcpys as util.c:275, chunk id mod 4 -> 4 verifiers on this GPU, one receive thread "
-            "each, 2 rounds timed after 1 untimed")
+            vs, ["-g", "4", "-t", "-b", "256", "-s", "2", "-r", "3", "-w", "1", img, lst])
     return out
 
 
@@ -899,9 +886,8 @@ def main():
         if ok:
             slow = min(range(world), key=lambda r: rank_mhz[r] if rank_mhz[r] is not None else math.inf)
             clock = {"in_kernel_mhz": min(ok), "probe_digests_identical": all(s > 0 for _, s in allc),
-                     "method": "stamped build of the hot kernel (bt_sha1_clock_probe): median over waves of "
-                               "delta s_memtime / delta s_memrealtime x wall-clock rate, 3 launches after the "
-                               "timed region, on every rank"}
+                     "method": "stamped hot kernel (bt_sha1_clock_probe): median over waves of d(s_memtime) / "
+                               "d(s_memrealtime) x wall-clock rate, 3 launches after the timed region, every rank"}
             if world > 1:
                 clock.update(slowest_rank=slow, per_rank_mhz=rank_mhz,
                              note="in_kernel_mhz = the slowest rank's clock (it prices the VALU roofline)")
@@ -1055,9 +1041,8 @@ def main():
                 "peak_at_measured_clock": round(peak_at_clock, 2) if peak_at_clock else None,
                 "frac_at_measured_clock": round(valu_tops / peak_at_clock, 4) if peak_at_clock else None,
                 "ops_per_block": VALU_OPS_PER_BLOCK,
-                "peak_basis": f"{VALU_OPS_PER_BLOCK}-instruction mix ({VALU_HALF_RATE_PER_BLOCK} half-rate, "
-                              f"{VALU_FULL_RATE_PER_BLOCK} full-rate) on 1024 SIMDs at 2.4 GHz (peak) and at the "
-                              "in-kernel clock (peak_at_measured_clock)"},
+                "peak_basis": f"{VALU_OPS_PER_BLOCK}-op mix ({VALU_HALF_RATE_PER_BLOCK} half-rate) on 1024 SIMDs "
+                              "at 2.4 GHz / at the in-kernel clock"},
             "clock": clock,
             "power": power,
             # per rank: its rate and kernel time, and which GPU it was (PCI address,

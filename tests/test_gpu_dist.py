@@ -249,27 +249,27 @@ def test_bench_host_path_leg_explains_itself(oracle):
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     hp = line["host_path"]
     assert hp["image_GiB"] == 1.0
+    assert hp["fields"] and len(json.dumps(line)) < 8000  # the whole line stays compact
     for key in ("pageable_chunks_host", "pageable_staged_copy", "registered_direct_dma"):
         p = hp[key]
-        assert p["digests_match"] is True and len(p["runs"]) == 6, p
-        steady = sorted(x["GiB_per_s"] for x in p["runs"][1:])
-        assert p["GiB_per_s"] == round(steady[2], 3) and p["steady_min_max"] == [steady[0], steady[-1]]
-        for run in p["runs"]:
-            assert run["s"] > 0 and run["wait_s"] >= 0 and run["fill_s"] >= 0 and run["cpu_s"] >= 0
+        runs = p["runs_GiB_per_s"]
+        assert p["digests_match"] is True and len(runs) == 6, p
+        assert p["GiB_per_s"] == round(sorted(runs[1:])[2], 3) and p["first_run_GiB_per_s"] == runs[0]
+        for run in (p["median_run"], p["first_run"]):
+            assert run["s"] > 0 and run["wait_s"] >= 0 and run["fill_s"] >= 0
             assert run["fill_s"] + run["wait_s"] <= run["s"] * 1.05 + 1e-3
-        assert 0 <= p["median_run_phases"]["fill_frac"] <= 1.05
+        m = p["median_run"]
+        assert m["cpu_s"] >= 0 and 0 <= m["fill_frac"] <= 1.05 and m["lock_s"] >= 0 and m["unlock_s"] >= 0
         assert 0 < p["frac_of_raw_h2d"] < 1.2
     reg, stg = hp["pageable_chunks_host"]["numa"], hp["pageable_staged_copy"]["numa"]
-    assert reg["feed"] == "registered" and reg["registered_batches"] == reg["batches"] == 2
-    assert sum(reg["staging_pieces_per_cpu_node"]) == 0
-    assert stg["feed"] == "staged" and stg["registered_batches"] == 0
-    assert stg["numa_nodes"] >= 1 and len(stg["image_pages_per_node"]) == stg["numa_nodes"]
-    assert sum(stg["image_pages_per_node"]) > 0 and sum(stg["lane_pages_per_node"]) > 0
-    assert sum(stg["staging_pieces_per_cpu_node"]) > 0
+    assert reg["feed"] == "registered" and reg["locked_batches"] == [2, 2] and sum(reg["staging_pieces"]) == 0
+    assert stg["feed"] == "staged" and stg["locked_batches"] == [0, 2]
+    assert sum(stg["image_pages"]) > 0 and sum(stg["lane_pages"]) > 0 and sum(stg["staging_pieces"]) > 0
+    assert len(stg["image_pages"]) == len(stg["lane_pages"]) == len(stg["staging_pieces"]) >= 1
     if stg["policy"] in ("lanes", "gpu"):  # the lanes sit on the GPU's node
-        assert stg["lane_pages_per_node"][stg["gpu_node"]] == sum(stg["lane_pages_per_node"])
+        assert stg["lane_pages"][stg["gpu_node"]] == sum(stg["lane_pages"])
     for key, threads in (("zero_copy_verifier", 1), ("packetized_verifier", 1), ("packetized_verifier_4_threads", 4)):
         v = hp[key]
         assert v["digests_match"] is True and v["GiB_per_s"] > 0 and "error" not in v, (key, v)
-        assert v["receive_threads"] == threads
+        assert v["receive_threads"] == threads and v["args"]
     assert hp["packetized_verifier"]["timed_chunks"] == 2 * 2048

@@ -642,10 +642,9 @@ def timed_runs(fn, want, gib, steady=5, stats=None):
 
 
 HOST_PATH_FIELDS = (
-    "GiB_per_s = median of runs 2-6 (runs_GiB_per_s: all 6); median_run / first_run: s wall, cpu_s process CPU, "
-    "throttled_s cgroup throttling, host_busy whole-machine CPU busy, fill_s host-side input (copies), wait_s "
-    "blocked on the GPU lane, lock_s / unlock_s page locking, fill_frac = fill_s / s; numa: feed, locked/all "
-    "batches, GPU node, image / lane pages and staging pieces per node, placement")
+    "GiB_per_s: median of runs 2-6; median_run/first_run: s wall, cpu_s, throttled_s (cgroup), host_busy (whole "
+    "machine), fill_s (host input copies), wait_s (on the GPU lane), lock_s/unlock_s (page locking); numa: feed, "
+    "locked/all batches, GPU node, image/lane pages and staging pieces per node")
 
 
 def numa_view(st):
@@ -708,6 +707,7 @@ def host_paths(bt, torch, dev_buf, host, want, verify_gib=1):  # noqa: C901
         out["registered_direct_dma"] = {
             **timed_runs(lambda: bt.chunks_host_addr(addr, nbytes), want, gib, stats=bt.pipeline_stats),
             "register_s": round(reg_s, 3)}
+        del out["registered_direct_dma"]["first_run"]  # nothing one-time left: the caller registered the image
         pin = torch.from_numpy(host)
         scratch = torch.empty(nbytes, dtype=torch.uint8, device=dev_buf.device)
         rates = []

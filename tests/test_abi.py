@@ -257,3 +257,34 @@ def test_make_install_tree_links_a_reference_style_caller(tmp_path):
     assert f"{prefix}/lib/libbtsha1.so" in ldd
     ldd = subprocess.run(["ldd", str(prefix / "bin" / "make-chunks")], capture_output=True, text=True).stdout
     assert f"{prefix}/lib/libbtsha1.so" in ldd
+
+
+@pytest.mark.parametrize("args,msg", [
+    (["-r", "2", "-w", "2"], "no timed round"),
+    (["-r", "0"], "usage"),
+    (["-g", "65"], "usage"),
+    (["-w", "-1"], "usage"),
+    (["-q"], "usage"),
+])
+def test_verify_stream_rejects_bad_options_before_any_gpu_call(tmp_path, args, msg):
+    """bin/verify-stream's option checks (-w warm-up rounds must leave a timed
+    round, -r >= 1, 1 <= -g <= 64) fail with status 255 and a message before
+    the data files are opened or a device is touched -- so they hold on a
+    machine without a GPU."""
+    exe = os.path.join(PKG, "bin", "verify-stream")
+    assert os.path.exists(exe), "run make tools first"
+    r = subprocess.run([exe, *args, str(tmp_path / "missing.img"), str(tmp_path / "missing.chunks")],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 255 and msg in r.stderr, (r.returncode, r.stderr)
+
+
+def test_pageable_feed_switch_needs_no_device():
+    """bt_sha1_set_pageable_feed: REGISTER (0, the default) / STAGE (1) swap
+    and report the previous setting; anything else is -1 with a message; no
+    device call is made."""
+    bt = load_btsha1()
+    prev = bt.set_pageable_feed("stage")
+    assert prev in ("register", "stage")
+    assert bt.set_pageable_feed("register") == "stage"
+    assert bt.lib.bt_sha1_set_pageable_feed(7) == -1 and "BT_SHA1_PAGEABLE_STAGE" in bt.last_error()
+    bt.set_pageable_feed(prev)

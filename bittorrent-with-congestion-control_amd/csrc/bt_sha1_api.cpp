@@ -907,9 +907,9 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   // cannot be registered (read-only, registered by the caller elsewhere) are
   // staged through the lane instead.  Every batch is locked before the first
   // copy is queued (pages locked before: ~0.1 ms per 8 GiB; never locked:
-  // 66-86 ms per 8 GiB of the bench's image however the locking is placed --
-  // per batch ahead of its DMA, on a helper thread, or all up front --
-  // profiles/r06; up front is the simplest).
+  // 14-22 ms per 8 GiB under the ROCm 7.2 runtime, 69-92 ms under the 7.0
+  // runtime torch bundles, however the locking is placed -- per batch ahead
+  // of its DMA, on a helper thread, or all up front; profiles/r06).
   const uint64_t batch = batch_bytes_for(chunk_len, total, false);
   const size_t nbatch = feed == Feed::kRegistered ? (size_t)((total + batch - 1) / batch) : 0;
   std::vector<uint64_t> bp0(nbatch), bp1(nbatch);

@@ -363,6 +363,8 @@ struct DevCtx {
   hipStream_t s = nullptr;  // drop-in calls and NULL-stream launches (= lane[0].s)
   Lane lane[2];
   PinBuf h_msg, h_state;  // drop-in calls: message / chaining state, read and written by the chain kernel
+  PinBuf h_zdig;          // host pipelines: digests of the zero-copy tail (registered feed)
+  hipEvent_t zev = nullptr;  // after the zero-copy tail's kernel
   uint32_t seq = 0;       // drop-in calls: completion word the chain kernel stores at h_state + 32
 };
 
@@ -425,6 +427,9 @@ void release_ctx(DevCtx *c) {
   c->s = nullptr;
   c->h_msg.release();
   c->h_state.release();
+  c->h_zdig.release();
+  if (c->zev) (void)hipEventDestroy(c->zev);
+  c->zev = nullptr;
 }
 
 // Streams are created on first use and kept few: HIP multiplexes streams onto
@@ -688,8 +693,11 @@ enum class Feed {
   kRegistered  // pageable caller memory page-locked batch by batch (chunks_host_on)
 };
 
-template <class Fill, class Sink>
-int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed feed, Fill fill, Sink sink) {
+// tail(stream): queued once every batch is, on the lane stream that is not
+// carrying the last batch (its previous batch's hash ends while the last copy
+// runs) -- the registered feed's zero-copy tail (chunks_host_on); 0 or -1.
+template <class Fill, class Sink, class Tail>
+int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed feed, Fill fill, Sink sink, Tail tail) {
   if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
     set_err("chunk_len must be in [1, 4 GiB)");
     return -1;
@@ -808,6 +816,7 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
     if (eof) break;
   }
   if (join_pre()) return -1;  // input shorter than the size hint
+  if (tail(c->lane[k & 1].s)) return -1;
   // Older lane first so digests arrive in order.
   if (drain(c->lane[k & 1]) || drain(c->lane[(k + 1) & 1])) return -1;
   // Direct-DMA batches bigger than a staged batch (BT_SHA1_DMA_BATCH_MB >
@@ -870,6 +879,19 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
 // path runs at the registered-image rate.  Inputs under kRegisterMin stay
 // staged (a few ms of copying at most).
 constexpr uint64_t kRegisterMin = 64ull << 20;
+constexpr uint64_t kZeroCopyDefault = 512;
+// Zero-copy tail of the registered feed: chunks hashed straight from host
+// memory at the end of a call (BT_SHA1_ZC_TAIL overrides; 0 = off), for
+// chunks of at least kZeroCopyMinChunk (a chain's latency scales with them).
+constexpr uint64_t kZeroCopyMinChunk = 64ull << 10;
+uint64_t zc_chunks() {
+  static const uint64_t v = [] {
+    const char *e = getenv("BT_SHA1_ZC_TAIL");
+    const long x = e ? atol(e) : (long)kZeroCopyDefault;
+    return (uint64_t)(x < 0 ? 0 : (x > 4096 ? 4096 : x));
+  }();
+  return v;
+}
 std::atomic<int> g_pageable_feed{-1};  // BT_SHA1_PAGEABLE_REGISTER / _STAGE; -1: not read yet
 int pageable_feed() {
   int v = g_pageable_feed.load();
@@ -910,8 +932,48 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   // 14-22 ms per 8 GiB under the ROCm 7.2 runtime, 69-92 ms under the 7.0
   // runtime torch bundles, however the locking is placed -- per batch ahead
   // of its DMA, on a helper thread, or all up front; profiles/r06).
-  const uint64_t batch = batch_bytes_for(chunk_len, total, false);
-  const size_t nbatch = feed == Feed::kRegistered ? (size_t)((total + batch - 1) / batch) : 0;
+  //
+  // Zero-copy tail (registered feed): the pipeline's last chunks can only be
+  // hashed after their copy, so it ends one chain latency (~6-7 ms) after
+  // the last byte crossed PCIe.  The last zc_chunks() chunks are therefore not
+  // copied: the chain kernel hashes them straight from the locked host pages
+  // (S reads each message over PCIe; no read strays past a message's end),
+  // launched while the last batch's copy is still running -- its reads and
+  // the copy share the link (tools/zero_copy_probe.py: 512 chunks hashed from
+  // host memory in 6.1 ms alone, 57.6 GB/s together with a 4 GiB copy, as
+  // the copy alone).  Its pages -- [floor_page(zc_off), ceil_page(total)),
+  // edges included, since the kernel reads them -- are locked as one range.
+  const uint64_t nchunks = (total + chunk_len - 1) / chunk_len, rem = total % chunk_len;
+  uint64_t zc_off = total, zc_msgs = 0;  // zero-copy region [zc_off, total): zc_msgs messages, the last maybe short
+  void *zc_lock = nullptr;
+  const uint8_t *zc_dev = nullptr;  // the region's address on the device
+  const double t_lock0 = now_s();
+  if (feed == Feed::kRegistered && chunk_len >= kZeroCopyMinChunk) {
+    const uint64_t want = std::min<uint64_t>(zc_chunks(), nchunks / 4);
+    if (want) {
+      const uintptr_t base = (uintptr_t)h_in;
+      const uint64_t off0 = (nchunks - want) * chunk_len;
+      const uintptr_t lo = (base + off0) & ~(uintptr_t)(kPage - 1);
+      const uintptr_t hi = (base + total + kPage - 1) & ~(uintptr_t)(kPage - 1);
+      void *dptr = nullptr;
+      if (hipHostRegister((void *)lo, (size_t)(hi - lo), hipHostRegisterPortable) == hipSuccess) {
+        if (hipHostGetDevicePointer(&dptr, (void *)(h_in + off0), 0) == hipSuccess && dptr) {
+          zc_lock = (void *)lo;
+          zc_dev = (const uint8_t *)dptr;
+          zc_off = off0;
+          zc_msgs = want;
+        } else {  // no device address for it: unlock, copy it with the rest
+          (void)hipGetLastError();
+          (void)hipHostUnregister((void *)lo);
+        }
+      } else {
+        (void)hipGetLastError();  // copied with the rest
+      }
+    }
+  }
+  const uint64_t dma_total = zc_off;  // the part that is copied
+  const uint64_t batch = batch_bytes_for(chunk_len, dma_total, false);
+  const size_t nbatch = feed == Feed::kRegistered ? (size_t)((dma_total + batch - 1) / batch) : 0;
   std::vector<uint64_t> bp0(nbatch), bp1(nbatch);
   std::vector<char> blocked(nbatch, 0);
   // Locked ranges stay locked until the whole call is done: hipHostUnregister
@@ -931,12 +993,13 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
       for (void *p : regs) (void)hipHostUnregister(p);
     }
   } unlock_at_exit{c, regs};
-  double lock_s = 0;
+  if (zc_lock) regs.push_back(zc_lock);
+  double lock_s = now_s() - t_lock0;
   if (nbatch) {
     const double t0 = now_s();
     const uintptr_t base = (uintptr_t)h_in;
     for (size_t k = 0; k < nbatch; ++k) {
-      const uint64_t lo = k * batch, hi = std::min<uint64_t>(lo + batch, total);
+      const uint64_t lo = k * batch, hi = std::min<uint64_t>(lo + batch, dma_total);
       bp0[k] = ((base + lo + kPage - 1) & ~(uintptr_t)(kPage - 1)) - base;
       bp1[k] = ((base + hi) & ~(uintptr_t)(kPage - 1)) - base;
       if (bp1[k] <= bp0[k]) {
@@ -950,12 +1013,12 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
         (void)hipGetLastError();  // that batch is staged
       }
     }
-    lock_s = now_s() - t0;
+    lock_s += now_s() - t0;
   }
   uint64_t b1 = 0, p0 = 0, p1 = 0;
   bool locked = false;
   auto fill = [&](Lane &l, uint64_t at, uint64_t max, const uint8_t **src, bool *eof) -> int64_t {
-    uint64_t n = std::min<uint64_t>(max, total - off);
+    uint64_t n = std::min<uint64_t>(max, dma_total - off);
     if (feed == Feed::kDirect) {
       *src = h_in + off;  // DMA straight from the caller's pinned image
     } else if (feed == Feed::kStaged) {
@@ -966,7 +1029,7 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
         const size_t k = (size_t)(off / batch);
         p0 = bp0[k];
         p1 = bp1[k];
-        b1 = std::min<uint64_t>((k + 1) * batch, total);
+        b1 = std::min<uint64_t>((k + 1) * batch, dma_total);
         locked = blocked[k] != 0;
       }
       uint8_t *edge = l.h_edge.as<uint8_t>();
@@ -990,23 +1053,51 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
       }
     }
     off += n;
-    *eof = off == total;
+    *eof = off == dma_total;
     return (int64_t)n;
   };
 
   auto sink = [&](uint64_t first, uint64_t count, const uint8_t *d) { memcpy(h_dig + 20 * first, d, 20 * count); };
-  const int64_t n = run_pipeline(c, chunk_len, total, feed, fill, sink);
+  bool zc_queued = false;
+  auto tail = [&](hipStream_t s) -> int {
+    if (!zc_msgs) return 0;
+    if (c->h_zdig.ensure(20 * zc_msgs)) return -1;
+    if (!c->zev) BT_CK(hipEventCreateWithFlags(&c->zev, hipEventDisableTiming));
+    const uint64_t full = rem ? zc_msgs - 1 : zc_msgs;
+    BT_CK(btsha1_launch_chain(zc_dev, nullptr, nullptr, chunk_len, chunk_len, full, c->h_zdig.as<uint8_t>(), s, rem,
+                              nullptr, nullptr));
+    BT_CK(hipEventRecord(c->zev, s));
+    zc_queued = true;
+    return 0;
+  };
+  int64_t n = run_pipeline(c, chunk_len, dma_total, feed, fill, sink, tail);
+  if (n >= 0 && zc_queued) {  // the zero-copy tail's digests follow the copied chunks'
+    const double t0 = now_s();
+    if (hipEventSynchronize(c->zev) != hipSuccess) {
+      set_err("zero-copy tail: %s", hipGetErrorString(hipGetLastError()));
+      n = -1;
+    } else {
+      memcpy(h_dig + 20 * (uint64_t)n, c->h_zdig.p, 20 * zc_msgs);
+      n += (int64_t)zc_msgs;
+      if (t_stats_valid) {
+        t_stats.chunks = (uint64_t)n;
+        t_stats.zero_copy_chunks = (uint32_t)zc_msgs;
+        t_stats.wait_s += now_s() - t0;
+        t_stats.total_s += now_s() - t0;
+      }
+    }
+  }
   if (n >= 0 && t_stats_valid) {
     t_stats.bytes = total;
     page_nodes(h_in, total, 64, t_stats.src_pages, BT_SHA1_STATS_NODES);
   }
-  if (n >= 0 && feed == Feed::kRegistered) {  // every batch is done: release the pages (timed into the stats)
+  if (n >= 0 && (feed == Feed::kRegistered || zc_lock)) {  // every batch is done: release the pages (timed)
     const double t0 = now_s();
     for (void *p : regs)
       if (hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
     const double dt = now_s() - t0;
     if (t_stats_valid) {
-      t_stats.registered_batches = (int32_t)regs.size();
+      t_stats.registered_batches = (int32_t)(regs.size() - (zc_lock ? 1 : 0));
       t_stats.register_s = lock_s;
       t_stats.unregister_s = dt;
       t_stats.total_s += lock_s + dt;
@@ -1067,7 +1158,7 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
     if (r > 0) bytes_in += (uint64_t)r;
     return r;
   };
-  const int64_t n = run_pipeline(c, chunk_len, hint, Feed::kStaged, counted_fill, sink);
+  const int64_t n = run_pipeline(c, chunk_len, hint, Feed::kStaged, counted_fill, sink, [](hipStream_t) { return 0; });
   if (n >= 0 && t_stats_valid) t_stats.bytes = bytes_in;
   if (regular) {
     // Leave the stream where the reference's fread loop leaves it: at EOF,

@@ -594,8 +594,10 @@ def test_pipeline_stats_account_for_each_host_run(bt, oracle, tmp_path):
     wall = time.perf_counter() - t0
     s = bt.pipeline_stats()
     assert (s["chunks"], s["bytes"], s["feed"], s["staged"]) == (151, data.nbytes, "registered", False)
-    assert s["batches"] == 2 and s["batch_bytes"] == 76 * CHUNK  # a 64 MiB - 2 GiB input: two batches
-    assert s["registered_batches"] == 2 and s["register_s"] >= 0
+    # the last min(512, n/4) chunks (the short one included) are hashed zero-copy
+    # from the locked pages; the other 114 (57 MiB, one batch) are copied
+    assert s["zero_copy_chunks"] == 37 and s["batches"] == 1 and s["batch_bytes"] == 114 * CHUNK
+    assert s["registered_batches"] == 1 and s["register_s"] >= 0
     assert 0 < s["total_s"] <= wall and s["fill_s"] + s["wait_s"] + s["alloc_s"] <= s["total_s"] * 1.001
     assert sum(s["src_pages"]) > 0 and sum(s["copy_pieces"]) == 0   # nothing copied by the staging threads
     bt.host_register(addr, data.nbytes)  # nothing of the call left registered
@@ -603,6 +605,7 @@ def test_pipeline_stats_account_for_each_host_run(bt, oracle, tmp_path):
         assert bt.chunks_host_addr(addr, data.nbytes) == want
         d = bt.pipeline_stats()
         assert (d["chunks"], d["feed"], d["numa_policy"], d["registered_batches"]) == (151, "direct", "none", 0)
+        assert d["zero_copy_chunks"] == 0 and d["batches"] == 2  # the caller's own registration: all copied
         assert sum(d["copy_pieces"]) == 0 and sum(d["lane_pages"]) == 0
     finally:
         bt.host_unregister(addr)
@@ -634,7 +637,9 @@ def test_pageable_image_registered_batch_by_batch_at_every_alignment(bt, oracle)
         want = b"".join(oracle.hash_chunks(bytes(raw[shift:shift + n]), CHUNK))
         assert bt.chunks_host_addr(addr, n) == want, shift
         s = bt.pipeline_stats()
-        assert (s["feed"], s["registered_batches"], s["chunks"]) == ("registered", 2, 141), shift
+        # 35 zero-copy chunks (the short one included, at this odd start) + 106 copied in one batch
+        assert (s["feed"], s["registered_batches"], s["chunks"], s["zero_copy_chunks"]) == ("registered", 1, 141, 35), \
+            shift
         bt.host_register(addr, n)
         bt.host_unregister(addr)
 
@@ -663,21 +668,32 @@ def test_registered_feed_falls_back_to_staging_pages_it_cannot_lock(bt, oracle, 
     del ro
 
 
-def test_pageable_stage_knob_keeps_the_staged_feed(tmp_path):
+@pytest.mark.parametrize("env,feed,zc", [({"BT_SHA1_PAGEABLE": "stage"}, "staged", 0),
+                                         ({"BT_SHA1_ZC_TAIL": "0"}, "registered", 0),
+                                         ({"BT_SHA1_ZC_TAIL": "4000"}, "registered", 32),
+                                         ({"BT_SHA1_ZC_TAIL": "7"}, "registered", 7)])
+def test_pageable_feed_knobs(tmp_path, env, feed, zc):
     """BT_SHA1_PAGEABLE=stage: pageable input of any size is copied into the
-    staging lanes, as before round 6 (child process: the knob is read once)."""
+    staging lanes, as before round 6; BT_SHA1_ZC_TAIL sets how many final
+    chunks of the registered feed are hashed straight from the locked host
+    pages (0 = none, capped at a quarter of the input).  Child processes: the
+    knobs are read once.  130 chunks + 77 bytes from an odd start."""
     code = (
         "import sys, numpy as np; sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2]);"
         "import btsha1 as bt, py_oracle as o;"
-        "d = np.frombuffer(bytes(o.fill_synthetic(130 * 524288 + 77, 3, 0x5EED)), dtype=np.uint8).copy();"
+        "raw = np.frombuffer(bytes(o.fill_synthetic(130 * 524288 + 77 + 4096, 3, 0x5EED)), dtype=np.uint8).copy();"
+        "k = (-raw.ctypes.data) % 4096 + 5; d = raw[k:k + 130 * 524288 + 77];"
         "w = b''.join(o.hash_chunks(bytes(d), 524288));"
         "assert bt.chunks_host_addr(d.ctypes.data, d.nbytes) == w;"
-        "s = bt.pipeline_stats(); assert s['feed'] == 'staged' and sum(s['copy_pieces']) > 0, s;"
-        "print('ok', s['batches'])")
-    env = dict(os.environ, BT_SHA1_PAGEABLE="stage")
+        "s = bt.pipeline_stats();"
+        "print('feed', s['feed'], 'zc', s['zero_copy_chunks'], 'chunks', s['chunks'], 'pieces', sum(s['copy_pieces']))")
     r = subprocess.run([sys.executable, "-c", code, PKG, os.path.join(REPO, "oracle")], capture_output=True,
-                       text=True, env=env, timeout=120)
-    assert r.returncode == 0 and "ok 2" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
+                       text=True, env=dict(os.environ, **env), timeout=120)
+    assert r.returncode == 0, (r.stdout[-1000:], r.stderr[-2000:])
+    out = r.stdout.split()
+    got = dict(zip(out[::2], out[1::2]))
+    assert (got["feed"], int(got["zc"]), int(got["chunks"])) == (feed, zc, 131), r.stdout
+    assert (int(got["pieces"]) > 0) == (feed == "staged")
 
 
 def test_registered_host_image_direct_dma(bt, oracle):

@@ -364,6 +364,8 @@ struct DevCtx {
   Lane lane[2];
   PinBuf h_msg, h_state;  // drop-in calls: message / chaining state, read and written by the chain kernel
   PinBuf h_zdig;          // host pipelines: digests of the zero-copy tail (registered feed)
+  PinBuf h_zlast;         //   its last chunk (copied: its page may reach past the input)
+  PinBuf h_zmeta;         //   its per-message offsets (uint64) and lengths (uint32), read by the kernel
   hipEvent_t zev = nullptr;  // after the zero-copy tail's kernel
   uint32_t seq = 0;       // drop-in calls: completion word the chain kernel stores at h_state + 32
 };
@@ -428,6 +430,8 @@ void release_ctx(DevCtx *c) {
   c->h_msg.release();
   c->h_state.release();
   c->h_zdig.release();
+  c->h_zlast.release();
+  c->h_zmeta.release();
   if (c->zev) (void)hipEventDestroy(c->zev);
   c->zev = nullptr;
 }
@@ -534,6 +538,9 @@ bool is_pinned(const void *p) {
   }
   return a.type == hipMemoryTypeHost;
 }
+// An input is DMA'd in place only when both its ends are pinned (a lock
+// around its first bytes alone -- a neighbour's page -- does not make it so).
+bool is_pinned_range(const uint8_t *p, uint64_t n) { return n && is_pinned(p) && is_pinned(p + n - 1); }
 
 // Workers of one bt_sha1_chunks_host_devices call (each a host thread with two
 // staging lanes of up to 1 GiB pinned + 1 GiB HBM while the call runs).
@@ -693,9 +700,10 @@ enum class Feed {
   kRegistered  // pageable caller memory page-locked batch by batch (chunks_host_on)
 };
 
-// tail(stream): queued once every batch is, on the lane stream that is not
-// carrying the last batch (its previous batch's hash ends while the last copy
-// runs) -- the registered feed's zero-copy tail (chunks_host_on); 0 or -1.
+// tail(stream, last_copied): queued once every batch is, on the lane stream
+// that is not carrying the last batch, with the event after the last batch's
+// copy (NULL when copies may overlap) -- the registered feed's zero-copy
+// tail (chunks_host_on); 0 or -1.
 template <class Fill, class Sink, class Tail>
 int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed feed, Fill fill, Sink sink, Tail tail) {
   if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
@@ -799,7 +807,14 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
       const int64_t r = fill(l, got, want, &src, &eof);
       t_fill += now_s() - t0;
       if (r < 0) return -1;
-      if (r) BT_CK(hipMemcpyAsync(l.d_in.as<uint8_t>() + got, src, (size_t)r, hipMemcpyHostToDevice, l.s));
+      if (r) {
+        const hipError_t ce = hipMemcpyAsync(l.d_in.as<uint8_t>() + got, src, (size_t)r, hipMemcpyHostToDevice, l.s);
+        if (ce != hipSuccess) {
+          set_err("hipMemcpyAsync of %llu bytes from host %p (batch %d, byte %llu of it) failed: %s",
+                  (unsigned long long)r, (const void *)src, k, (unsigned long long)got, hipGetErrorString(ce));
+          return -1;
+        }
+      }
       got += (uint64_t)r;
       if (r == 0) eof = true;
     }
@@ -816,7 +831,7 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
     if (eof) break;
   }
   if (join_pre()) return -1;  // input shorter than the size hint
-  if (tail(c->lane[k & 1].s)) return -1;
+  if (tail(c->lane[k & 1].s, k > 0 && serial_copies(staged) ? c->lane[(k + 1) & 1].copied : nullptr)) return -1;
   // Older lane first so digests arrive in order.
   if (drain(c->lane[k & 1]) || drain(c->lane[(k + 1) & 1])) return -1;
   // Direct-DMA batches bigger than a staged batch (BT_SHA1_DMA_BATCH_MB >
@@ -917,7 +932,7 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
     set_err("hipSetDevice(%d) failed", dev);
     return -1;
   }
-  const bool pinned = is_pinned(h_in);
+  const bool pinned = is_pinned_range(h_in, total);
   const Feed feed = pinned ? Feed::kDirect
                     : (register_pageable() && total >= kRegisterMin) ? Feed::kRegistered
                                                                       : Feed::kStaged;
@@ -936,32 +951,60 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   // Zero-copy tail (registered feed): the pipeline's last chunks can only be
   // hashed after their copy, so it ends one chain latency (~6-7 ms) after
   // the last byte crossed PCIe.  The last zc_chunks() chunks are therefore not
-  // copied: the chain kernel hashes them straight from the locked host pages
-  // (S reads each message over PCIe; no read strays past a message's end),
-  // launched while the last batch's copy is still running -- its reads and
-  // the copy share the link (tools/zero_copy_probe.py: 512 chunks hashed from
-  // host memory in 6.1 ms alone, 57.6 GB/s together with a 4 GiB copy, as
-  // the copy alone).  Its pages -- [floor_page(zc_off), ceil_page(total)),
-  // edges included, since the kernel reads them -- are locked as one range.
+  // copied: the chain kernel hashes them straight from host memory (S reads
+  // each message over PCIe; no read strays past a message's end), queued to
+  // start when the last batch's copy is done, so their reads run while that
+  // batch hashes (tools/zero_copy_probe.py: 512 chunks hashed from host
+  // memory in 6.1 ms, at the chain's latency).  The kernel reads every byte
+  // of its messages, so all their pages must be locked -- but never a page
+  // past the input: the page holding the input's end may belong to whatever
+  // follows it (another worker's slice, another call's buffer), and a lock
+  // there makes that memory look registered to it.  So the tail's messages
+  // that end before the input's last page boundary are read in place from
+  // [floor_page(zc_off), that boundary's chunk end) -- whole pages inside
+  // the input -- and the one or two chunks reaching past it are copied into a
+  // pinned buffer and read from there, in the same launch (per-message
+  // offsets from the tail's base, lengths).
   const uint64_t nchunks = (total + chunk_len - 1) / chunk_len, rem = total % chunk_len;
+  const uint64_t last_len = rem ? rem : chunk_len;
   uint64_t zc_off = total, zc_msgs = 0;  // zero-copy region [zc_off, total): zc_msgs messages, the last maybe short
   void *zc_lock = nullptr;
   const uint8_t *zc_dev = nullptr;  // the region's address on the device
   const double t_lock0 = now_s();
   if (feed == Feed::kRegistered && chunk_len >= kZeroCopyMinChunk) {
     const uint64_t want = std::min<uint64_t>(zc_chunks(), nchunks / 4);
-    if (want) {
-      const uintptr_t base = (uintptr_t)h_in;
-      const uint64_t off0 = (nchunks - want) * chunk_len;
-      const uintptr_t lo = (base + off0) & ~(uintptr_t)(kPage - 1);
-      const uintptr_t hi = (base + total + kPage - 1) & ~(uintptr_t)(kPage - 1);
-      void *dptr = nullptr;
+    const uintptr_t base = (uintptr_t)h_in;
+    const uint64_t off0 = (nchunks - want) * chunk_len;
+    const uint64_t bound = ((base + total) & ~(uintptr_t)(kPage - 1)) - base;  // the input's last page boundary
+    const uint64_t q = bound / chunk_len;  // chunks [0, q) end at or before it
+    const uintptr_t lo = (base + off0) & ~(uintptr_t)(kPage - 1);
+    const uintptr_t hi = (base + q * chunk_len + kPage - 1) & ~(uintptr_t)(kPage - 1);
+    const uint64_t copied = total - q * chunk_len;  // bytes of the chunks [q, nchunks): at most two
+    if (want >= 2 && q > nchunks - want && lo >= base && hi <= base + bound && hi > lo &&
+        !c->h_zlast.ensure(copied) && !c->h_zmeta.ensure(12 * want)) {
+      void *dptr = nullptr, *lptr = nullptr;
       if (hipHostRegister((void *)lo, (size_t)(hi - lo), hipHostRegisterPortable) == hipSuccess) {
-        if (hipHostGetDevicePointer(&dptr, (void *)(h_in + off0), 0) == hipSuccess && dptr) {
+        if (hipHostGetDevicePointer(&dptr, (void *)(h_in + off0), 0) == hipSuccess && dptr &&
+            hipHostGetDevicePointer(&lptr, c->h_zlast.p, 0) == hipSuccess && lptr) {
+          if (trace_on())
+            fprintf(stderr, "libbtsha1 lock zero-copy tail: [%p, %p), %llu chunks (%llu copied)\n", (void *)lo,
+                    (void *)hi, (unsigned long long)want, (unsigned long long)(nchunks - q));
           zc_lock = (void *)lo;
           zc_dev = (const uint8_t *)dptr;
           zc_off = off0;
           zc_msgs = want;
+          // message i (chunk nchunks - want + i) at zc_dev + offsets[i] -- the
+          // copied ones in the pinned buffer, their offsets wrapping modulo
+          // 2^64 -- of lengths[i] bytes
+          uint64_t *offs = c->h_zmeta.as<uint64_t>();
+          uint32_t *lens = (uint32_t *)(offs + want);
+          for (uint64_t i = 0; i < want; ++i) {
+            const uint64_t chunk = nchunks - want + i;
+            offs[i] = chunk < q ? i * chunk_len
+                                : (uint64_t)((uintptr_t)lptr + (chunk - q) * chunk_len - (uintptr_t)dptr);
+            lens[i] = (uint32_t)(chunk + 1 < nchunks ? chunk_len : last_len);
+          }
+          memcpy(c->h_zlast.p, h_in + q * chunk_len, copied);
         } else {  // no device address for it: unlock, copy it with the rest
           (void)hipGetLastError();
           (void)hipHostUnregister((void *)lo);
@@ -1009,6 +1052,9 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
       if (hipHostRegister((void *)(h_in + bp0[k]), (size_t)(bp1[k] - bp0[k]), hipHostRegisterPortable) == hipSuccess) {
         regs.push_back((void *)(h_in + bp0[k]));
         blocked[k] = 1;
+        if (trace_on())
+          fprintf(stderr, "libbtsha1 lock batch %zu: [%p, %p)\n", k, (const void *)(h_in + bp0[k]),
+                  (const void *)(h_in + bp1[k]));
       } else {
         (void)hipGetLastError();  // that batch is staged
       }
@@ -1059,13 +1105,16 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
 
   auto sink = [&](uint64_t first, uint64_t count, const uint8_t *d) { memcpy(h_dig + 20 * first, d, 20 * count); };
   bool zc_queued = false;
-  auto tail = [&](hipStream_t s) -> int {
+  auto tail = [&](hipStream_t s, hipEvent_t last_copied) -> int {
     if (!zc_msgs) return 0;
+    // after the last batch's copy: the tail's reads then run while that
+    // batch hashes instead of slowing its copy
+    if (last_copied) BT_CK(hipStreamWaitEvent(s, last_copied, 0));
     if (c->h_zdig.ensure(20 * zc_msgs)) return -1;
     if (!c->zev) BT_CK(hipEventCreateWithFlags(&c->zev, hipEventDisableTiming));
-    const uint64_t full = rem ? zc_msgs - 1 : zc_msgs;
-    BT_CK(btsha1_launch_chain(zc_dev, nullptr, nullptr, chunk_len, chunk_len, full, c->h_zdig.as<uint8_t>(), s, rem,
-                              nullptr, nullptr));
+    const uint64_t *offs = c->h_zmeta.as<uint64_t>();
+    BT_CK(btsha1_launch_chain(zc_dev, offs, (const uint32_t *)(offs + zc_msgs), 0, 0, zc_msgs,
+                              c->h_zdig.as<uint8_t>(), s, 0, nullptr, nullptr));
     BT_CK(hipEventRecord(c->zev, s));
     zc_queued = true;
     return 0;
@@ -1158,7 +1207,8 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
     if (r > 0) bytes_in += (uint64_t)r;
     return r;
   };
-  const int64_t n = run_pipeline(c, chunk_len, hint, Feed::kStaged, counted_fill, sink, [](hipStream_t) { return 0; });
+  const int64_t n = run_pipeline(c, chunk_len, hint, Feed::kStaged, counted_fill, sink,
+                                 [](hipStream_t, hipEvent_t) { return 0; });
   if (n >= 0 && t_stats_valid) t_stats.bytes = bytes_in;
   if (regular) {
     // Leave the stream where the reference's fread loop leaves it: at EOF,

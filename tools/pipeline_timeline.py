@@ -54,9 +54,10 @@ def summary(d):
 
     kern = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:40])
                    for r in rows("*kernel_trace.csv")), key=lambda x: x[0])
-    copies = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Direction", ""),
-                      int(r.get("Bytes", 0) or 0)) for r in rows("*memory_copy_trace.csv")), key=lambda x: x[0])
-    big = [c for c in copies if c[3] >= (64 << 20)]
+    copies = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Direction", ""))
+                     for r in rows("*memory_copy_trace.csv")), key=lambda x: x[0])
+    # the trace carries no byte counts: the pipeline's batch copies are the H2D ones over 1 ms
+    big = [c for c in copies if "HOST_TO_DEVICE" in c[2] and c[1] - c[0] > 1_000_000]
     # calls: runs of big H2D copies separated by > 50 ms
     groups, cur = [], []
     for c in big:
@@ -68,13 +69,10 @@ def summary(d):
         groups.append(cur)
     for gi, g in enumerate(groups):
         c0, c1 = g[0][0], g[-1][1]
-        nbytes = sum(c[3] for c in g)
         after = [k for k in kern if c0 <= k[1] and k[0] <= c1 + 100_000_000]
         tail = [k for k in after if k[1] > c1]
         end = max([c1] + [k[1] for k in tail])
-        line = {"call": gi, "copies": len(g), "copy_GiB": round(nbytes / 2**30, 3),
-                "copy_span_ms": round((c1 - c0) / 1e6, 3),
-                "copy_GiB_per_s": round(nbytes / ((c1 - c0) / 1e9) / 2**30, 2),
+        line = {"call": gi, "copies": len(g), "copy_span_ms": round((c1 - c0) / 1e6, 3),
                 "copy_gaps_ms": [round((g[i + 1][0] - g[i][1]) / 1e6, 3) for i in range(len(g) - 1)],
                 "copy_ms": [round((c[1] - c[0]) / 1e6, 3) for c in g],
                 "end_after_last_copy_ms": round((end - c1) / 1e6, 3),

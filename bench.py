@@ -644,14 +644,14 @@ def timed_runs(fn, want, gib, steady=5, stats=None):
 HOST_PATH_FIELDS = (
     "GiB_per_s: median of runs 2-6; median_run/first_run: s wall, cpu_s, throttled_s (cgroup), host_busy (whole "
     "machine), fill_s (host input copies), wait_s (on the GPU lane), lock_s/unlock_s (page locking); numa: feed, "
-    "locked/all batches, zero-copy tail chunks, GPU node, image/lane pages and staging pieces per node")
+    "locked/all batches, column-split tail chunks, GPU node, image/lane pages and staging pieces per node")
 
 
 def numa_view(st):
     """How a pipeline run was fed and where its memory sat, from
     bt_sha1_get_pipeline_stats (fields in HOST_PATH_FIELDS)."""
     return {"feed": st["feed"], "locked_batches": [st["registered_batches"], st["batches"]],
-            "zero_copy_chunks": st["zero_copy_chunks"],
+            "column_chunks": st["column_chunks"],
             "gpu_node": st["gpu_numa_node"], "image_pages": st["src_pages"], "lane_pages": st["lane_pages"],
             "staging_pieces": st["copy_pieces"], "policy": st["numa_policy"], "copy_threads": st["copy_threads"]}
 

@@ -48,7 +48,7 @@ class PipelineStats(ctypes.Structure):  # include/bt_sha1.h bt_sha1_pipeline_sta
                 ("batches", ctypes.c_uint32), ("staged", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("copy_threads", ctypes.c_int32), ("numa_nodes", ctypes.c_int32),
                 ("gpu_numa_node", ctypes.c_int32), ("numa_policy", ctypes.c_int32),
-                ("registered_batches", ctypes.c_int32), ("zero_copy_chunks", ctypes.c_uint32),
+                ("registered_batches", ctypes.c_int32), ("column_chunks", ctypes.c_uint32),
                 ("total_s", ctypes.c_double), ("alloc_s", ctypes.c_double), ("fill_s", ctypes.c_double),
                 ("wait_s", ctypes.c_double), ("register_s", ctypes.c_double), ("unregister_s", ctypes.c_double),
                 ("lane_pages", ctypes.c_int32 * STATS_NODES), ("src_pages", ctypes.c_int32 * STATS_NODES),

@@ -86,6 +86,8 @@ struct KeepDevice {
 };
 
 // Grow-only device / pinned scratch.
+constexpr uint32_t kMaxColumns = 16;  // column-split tail: most columns per chunk (chunks_host_on)
+
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
@@ -363,10 +365,14 @@ struct DevCtx {
   hipStream_t s = nullptr;  // drop-in calls and NULL-stream launches (= lane[0].s)
   Lane lane[2];
   PinBuf h_msg, h_state;  // drop-in calls: message / chaining state, read and written by the chain kernel
-  PinBuf h_zdig;          // host pipelines: digests of the zero-copy tail (registered feed)
-  PinBuf h_zlast;         //   its last chunk (copied: its page may reach past the input)
-  PinBuf h_zmeta;         //   its per-message offsets (uint64) and lengths (uint32), read by the kernel
-  hipEvent_t zev = nullptr;  // after the zero-copy tail's kernel
+  // Host pipelines' column-split last batch (chunks_host_on): its digests, its
+  // few chunks that are not split (hashed from a pinned copy), the chunks'
+  // chaining state between columns, the column and leftover streams, an event
+  // per column copy and one after each stream's work.
+  PinBuf h_cdig, h_cleft;
+  DevBuf d_cstate;
+  hipStream_t cs = nullptr, xs = nullptr;
+  hipEvent_t cev[kMaxColumns] = {}, cdone = nullptr, xdone = nullptr;
   uint32_t seq = 0;       // drop-in calls: completion word the chain kernel stores at h_state + 32
 };
 
@@ -429,11 +435,21 @@ void release_ctx(DevCtx *c) {
   c->s = nullptr;
   c->h_msg.release();
   c->h_state.release();
-  c->h_zdig.release();
-  c->h_zlast.release();
-  c->h_zmeta.release();
-  if (c->zev) (void)hipEventDestroy(c->zev);
-  c->zev = nullptr;
+  c->h_cdig.release();
+  c->h_cleft.release();
+  c->d_cstate.release();
+  for (hipEvent_t &e : c->cev) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+  }
+  for (hipEvent_t *e : {&c->cdone, &c->xdone}) {
+    if (*e) (void)hipEventDestroy(*e);
+    *e = nullptr;
+  }
+  for (hipStream_t *t : {&c->cs, &c->xs}) {
+    if (*t) (void)hipStreamDestroy(*t);
+    *t = nullptr;
+  }
 }
 
 // Streams are created on first use and kept few: HIP multiplexes streams onto
@@ -700,10 +716,24 @@ enum class Feed {
   kRegistered  // pageable caller memory page-locked batch by batch (chunks_host_on)
 };
 
-// tail(stream, last_copied): queued once every batch is, on the lane stream
-// that is not carrying the last batch, with the event after the last batch's
-// copy (NULL when copies may overlap) -- the registered feed's zero-copy
-// tail (chunks_host_on); 0 or -1.
+// tail.queue(idle_lane, last_copied): called once every batch is queued, with
+// the lane that is not carrying the last batch and the event after the last
+// batch's copy (NULL when copies may overlap) -- chunks_host_on's column-split
+// tail; tail.wait() after the lanes are drained, before any lane buffer is
+// resized.  Both return 0 or -1.
+template <class Q, class W>
+struct TailOps {
+  Q queue;
+  W wait;
+};
+template <class Q, class W>
+TailOps<Q, W> tail_ops(Q q, W w) {
+  return TailOps<Q, W>{q, w};
+}
+inline auto no_tail() {
+  return tail_ops([](Lane &, hipEvent_t) { return 0; }, [] { return 0; });
+}
+
 template <class Fill, class Sink, class Tail>
 int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed feed, Fill fill, Sink sink, Tail tail) {
   if (chunk_len == 0 || chunk_len >= (1ull << 32)) {
@@ -831,9 +861,14 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
     if (eof) break;
   }
   if (join_pre()) return -1;  // input shorter than the size hint
-  if (tail(c->lane[k & 1].s, k > 0 && serial_copies(staged) ? c->lane[(k + 1) & 1].copied : nullptr)) return -1;
+  if (tail.queue(c->lane[k & 1], k > 0 && serial_copies(staged) ? c->lane[(k + 1) & 1].copied : nullptr)) return -1;
   // Older lane first so digests arrive in order.
   if (drain(c->lane[k & 1]) || drain(c->lane[(k + 1) & 1])) return -1;
+  {
+    const double t0 = now_s();
+    if (tail.wait()) return -1;
+    t_wait += now_s() - t0;
+  }
   // Direct-DMA batches bigger than a staged batch (BT_SHA1_DMA_BATCH_MB >
   // 1024) are not kept past the call: the lanes keep at most 1 GiB of HBM
   // each, so a process that shares the GPU does not lose more for good.  An
@@ -894,16 +929,26 @@ int64_t run_pipeline(DevCtx *c, uint64_t chunk_len, uint64_t size_hint, Feed fee
 // path runs at the registered-image rate.  Inputs under kRegisterMin stay
 // staged (a few ms of copying at most).
 constexpr uint64_t kRegisterMin = 64ull << 20;
-constexpr uint64_t kZeroCopyDefault = 512;
-// Zero-copy tail of the registered feed: chunks hashed straight from host
-// memory at the end of a call (BT_SHA1_ZC_TAIL overrides; 0 = off), for
-// chunks of at least kZeroCopyMinChunk (a chain's latency scales with them).
-constexpr uint64_t kZeroCopyMinChunk = 64ull << 10;
-uint64_t zc_chunks() {
+// Column-split last batch (chunks_host_on): columns per chunk (8 by default;
+// BT_SHA1_COLUMNS overrides, 2..16, 0 or 1 = off), for chunks of at least
+// kColumnMinChunk (a chain's latency scales with the chunk) and a split part
+// of at least column_min_bytes() (256 MiB; BT_SHA1_COLUMN_MIN_MB overrides:
+// below that the columns' copies are shorter than the previous batch's hash,
+// which then ends the call anyway).
+constexpr uint64_t kColumnMinChunk = 64ull << 10;
+uint64_t column_min_bytes() {
   static const uint64_t v = [] {
-    const char *e = getenv("BT_SHA1_ZC_TAIL");
-    const long x = e ? atol(e) : (long)kZeroCopyDefault;
-    return (uint64_t)(x < 0 ? 0 : (x > 4096 ? 4096 : x));
+    const char *e = getenv("BT_SHA1_COLUMN_MIN_MB");
+    const long mb = e ? atol(e) : 256;
+    return (uint64_t)(mb < 0 ? 0 : mb) << 20;
+  }();
+  return v;
+}
+uint32_t columns() {
+  static const uint32_t v = [] {
+    const char *e = getenv("BT_SHA1_COLUMNS");
+    const long x = e ? atol(e) : 8;
+    return (uint32_t)(x < 2 ? 0 : (x > (long)kMaxColumns ? kMaxColumns : x));
   }();
   return v;
 }
@@ -948,73 +993,73 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   // runtime torch bundles, however the locking is placed -- per batch ahead
   // of its DMA, on a helper thread, or all up front; profiles/r06).
   //
-  // Zero-copy tail (registered feed): the pipeline's last chunks can only be
-  // hashed after their copy, so it ends one chain latency (~6-7 ms) after
-  // the last byte crossed PCIe.  The last zc_chunks() chunks are therefore not
-  // copied: the chain kernel hashes them straight from host memory (S reads
-  // each message over PCIe; no read strays past a message's end), queued to
-  // start when the last batch's copy is done, so their reads run while that
-  // batch hashes (tools/zero_copy_probe.py: 512 chunks hashed from host
-  // memory in 6.1 ms, at the chain's latency).  The kernel reads every byte
-  // of its messages, so all their pages must be locked -- but never a page
-  // past the input: the page holding the input's end may belong to whatever
-  // follows it (another worker's slice, another call's buffer), and a lock
-  // there makes that memory look registered to it.  So the tail's messages
-  // that end before the input's last page boundary are read in place from
-  // [floor_page(zc_off), that boundary's chunk end) -- whole pages inside
-  // the input -- and the one or two chunks reaching past it are copied into a
-  // pinned buffer and read from there, in the same launch (per-message
-  // offsets from the tail's base, lengths).
-  const uint64_t nchunks = (total + chunk_len - 1) / chunk_len, rem = total % chunk_len;
-  const uint64_t last_len = rem ? rem : chunk_len;
-  uint64_t zc_off = total, zc_msgs = 0;  // zero-copy region [zc_off, total): zc_msgs messages, the last maybe short
-  void *zc_lock = nullptr;
-  const uint8_t *zc_dev = nullptr;  // the region's address on the device
+  // Column-split last batch (registered and direct feeds).  A pipeline's last
+  // chunks can only be hashed once copied, and a chunk's hash is one serial
+  // chain (~6.8 ms per 512 KiB in k_sha1_lat), so an unsplit pipeline ends a
+  // chain latency after its last byte crossed PCIe (profiles/r06: 6.8 of the
+  // 158 ms an 8 GiB image takes).  The last ~batch of chunks is therefore
+  // copied COLUMN by column: columns() 2D copies (rows = the chunks, W =
+  // chunk_len / columns() bytes of each; the DMA engine runs them at the 1D
+  // rate, tools/copy2d_probe.py) into the idle lane's device buffer, column-
+  // major, each hashed by k_sha1_lat's column form (chaining state in HBM) as
+  // soon as it has arrived, on a stream of its own, while the next column
+  // crosses PCIe.  After the last byte only one column's W/64 blocks remain
+  // (~0.9 ms for 512 KiB chunks in 8 columns).  The copies read every byte of
+  // their rows, so with the registered feed those rows' pages are locked too
+  // -- but never a page reaching past the input (the page holding its end or
+  // start may belong to a neighbour: another worker's slice, another call's
+  // buffer); the one to three chunks touching such a page, and a short last
+  // chunk, are copied into a pinned buffer on the host and hashed from there
+  // by the chain kernel on a third stream, beside the columns.
+  const uint64_t nchunks = (total + chunk_len - 1) / chunk_len, nfull = total / chunk_len, rem = total % chunk_len;
+  struct Split {
+    uint64_t t0 = 0, c0 = 0, c1 = 0;  // the split tail: chunks [t0, nchunks); by columns: [c0, c1)
+    uint32_t parts = 0, width = 0;    // columns and their width
+    bool head = false;                // chunk t0 is a leftover (c0 == t0 + 1)
+    void *lock = nullptr;             // registered feed: the columns' locked pages
+  } sp;
   const double t_lock0 = now_s();
-  if (feed == Feed::kRegistered && chunk_len >= kZeroCopyMinChunk) {
-    const uint64_t want = std::min<uint64_t>(zc_chunks(), nchunks / 4);
+  if (feed != Feed::kStaged) {
+    uint32_t parts = columns();
+    while (parts >= 2 && chunk_len % (64ull * parts)) parts /= 2;
+    const uint64_t per = batch_bytes_for(chunk_len, total, false) / chunk_len;
+    const uint64_t t0 = nchunks - std::min<uint64_t>(nchunks, per);
+    uint64_t c0 = t0, c1 = nfull;
     const uintptr_t base = (uintptr_t)h_in;
-    const uint64_t off0 = (nchunks - want) * chunk_len;
-    const uint64_t bound = ((base + total) & ~(uintptr_t)(kPage - 1)) - base;  // the input's last page boundary
-    const uint64_t q = bound / chunk_len;  // chunks [0, q) end at or before it
-    const uintptr_t lo = (base + off0) & ~(uintptr_t)(kPage - 1);
-    const uintptr_t hi = (base + q * chunk_len + kPage - 1) & ~(uintptr_t)(kPage - 1);
-    const uint64_t copied = total - q * chunk_len;  // bytes of the chunks [q, nchunks): at most two
-    if (want >= 2 && q > nchunks - want && lo >= base && hi <= base + bound && hi > lo &&
-        !c->h_zlast.ensure(copied) && !c->h_zmeta.ensure(12 * want)) {
-      void *dptr = nullptr, *lptr = nullptr;
-      if (hipHostRegister((void *)lo, (size_t)(hi - lo), hipHostRegisterPortable) == hipSuccess) {
-        if (hipHostGetDevicePointer(&dptr, (void *)(h_in + off0), 0) == hipSuccess && dptr &&
-            hipHostGetDevicePointer(&lptr, c->h_zlast.p, 0) == hipSuccess && lptr) {
+    uintptr_t lo = 0, hi = 0;
+    if (feed == Feed::kRegistered) {
+      const uint64_t bound = ((base + total) & ~(uintptr_t)(kPage - 1)) - base;  // the input's last page boundary
+      c1 = std::min<uint64_t>(nfull, bound / chunk_len);  // chunks [0, c1) end at or before it
+      if (((base + c0 * chunk_len) & ~(uintptr_t)(kPage - 1)) < base) ++c0;  // t0 == 0, unaligned start
+      lo = (base + c0 * chunk_len) & ~(uintptr_t)(kPage - 1);
+      hi = (base + c1 * chunk_len + kPage - 1) & ~(uintptr_t)(kPage - 1);
+    }
+    if (parts >= 2 && chunk_len >= kColumnMinChunk && c1 > c0 + 1 && (c1 - c0) * chunk_len >= column_min_bytes() &&
+        !c->h_cdig.ensure(20 * (nchunks - t0 + 3)) && !c->h_cleft.ensure(3 * chunk_len) &&
+        !c->d_cstate.ensure(20 * (c1 - c0))) {
+      bool ok = true;
+      if (feed == Feed::kRegistered) {
+        ok = hipHostRegister((void *)lo, (size_t)(hi - lo), hipHostRegisterPortable) == hipSuccess;
+        if (ok) {
+          sp.lock = (void *)lo;
           if (trace_on())
-            fprintf(stderr, "libbtsha1 lock zero-copy tail: [%p, %p), %llu chunks (%llu copied)\n", (void *)lo,
-                    (void *)hi, (unsigned long long)want, (unsigned long long)(nchunks - q));
-          zc_lock = (void *)lo;
-          zc_dev = (const uint8_t *)dptr;
-          zc_off = off0;
-          zc_msgs = want;
-          // message i (chunk nchunks - want + i) at zc_dev + offsets[i] -- the
-          // copied ones in the pinned buffer, their offsets wrapping modulo
-          // 2^64 -- of lengths[i] bytes
-          uint64_t *offs = c->h_zmeta.as<uint64_t>();
-          uint32_t *lens = (uint32_t *)(offs + want);
-          for (uint64_t i = 0; i < want; ++i) {
-            const uint64_t chunk = nchunks - want + i;
-            offs[i] = chunk < q ? i * chunk_len
-                                : (uint64_t)((uintptr_t)lptr + (chunk - q) * chunk_len - (uintptr_t)dptr);
-            lens[i] = (uint32_t)(chunk + 1 < nchunks ? chunk_len : last_len);
-          }
-          memcpy(c->h_zlast.p, h_in + q * chunk_len, copied);
-        } else {  // no device address for it: unlock, copy it with the rest
-          (void)hipGetLastError();
-          (void)hipHostUnregister((void *)lo);
+            fprintf(stderr, "libbtsha1 lock column tail: [%p, %p)\n", (void *)lo, (void *)hi);
+        } else {
+          (void)hipGetLastError();  // copied with the rest
         }
-      } else {
-        (void)hipGetLastError();  // copied with the rest
+      }
+      if (ok) {
+        sp.t0 = t0;
+        sp.c0 = c0;
+        sp.c1 = c1;
+        sp.parts = parts;
+        sp.width = (uint32_t)(chunk_len / parts);
+        sp.head = c0 > t0;
       }
     }
+    t_err.clear();
   }
-  const uint64_t dma_total = zc_off;  // the part that is copied
+  const uint64_t dma_total = sp.parts ? sp.t0 * chunk_len : total;  // the part the lane batches carry
   const uint64_t batch = batch_bytes_for(chunk_len, dma_total, false);
   const size_t nbatch = feed == Feed::kRegistered ? (size_t)((dma_total + batch - 1) / batch) : 0;
   std::vector<uint64_t> bp0(nbatch), bp1(nbatch);
@@ -1023,20 +1068,24 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   // waits for the device's outstanding work, so releasing a batch's pages
   // while the next batch's copy and hash are in flight stalled the pipeline
   // (40.5 GiB/s instead of 50.7 on 8 GiB, profiles/r06).  At the end nothing
-  // is in flight and each release is quick; on an error path the lanes'
-  // streams are drained first.
+  // is in flight and each release is quick; on an error path the streams are
+  // drained first.
   std::vector<void *> regs;
-  struct UnlockAtExit {
+  bool split_queued = false;
+  struct DrainAtExit {
     DevCtx *c;
     std::vector<void *> &regs;
-    ~UnlockAtExit() {
-      if (regs.empty()) return;
+    bool &queued;
+    ~DrainAtExit() {
+      if (regs.empty() && !queued) return;
       for (auto &l : c->lane)
         if (l.s) (void)hipStreamSynchronize(l.s);
+      for (hipStream_t t : {c->cs, c->xs})
+        if (t) (void)hipStreamSynchronize(t);
       for (void *p : regs) (void)hipHostUnregister(p);
     }
-  } unlock_at_exit{c, regs};
-  if (zc_lock) regs.push_back(zc_lock);
+  } drain_at_exit{c, regs, split_queued};
+  if (sp.lock) regs.push_back(sp.lock);
   double lock_s = now_s() - t_lock0;
   if (nbatch) {
     const double t0 = now_s();
@@ -1060,6 +1109,14 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
       }
     }
     lock_s += now_s() - t0;
+  }
+  // The columns land in the lane that is idle once the last batch is queued
+  // (its previous batch's hash precedes them on its stream): sized for them
+  // up front, never grown while a batch may still read it.
+  if (sp.parts) {
+    const int k_last = dma_total ? (int)((dma_total + batch - 1) / batch) : 0;
+    if (c->lane[k_last & 1].d_in.ensure(std::max<uint64_t>((sp.c1 - sp.c0) * chunk_len, dma_total ? batch : 0)))
+      return -1;
   }
   uint64_t b1 = 0, p0 = 0, p1 = 0;
   bool locked = false;
@@ -1104,35 +1161,82 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   };
 
   auto sink = [&](uint64_t first, uint64_t count, const uint8_t *d) { memcpy(h_dig + 20 * first, d, 20 * count); };
-  bool zc_queued = false;
-  auto tail = [&](hipStream_t s, hipEvent_t last_copied) -> int {
-    if (!zc_msgs) return 0;
-    // after the last batch's copy: the tail's reads then run while that
-    // batch hashes instead of slowing its copy
-    if (last_copied) BT_CK(hipStreamWaitEvent(s, last_copied, 0));
-    if (c->h_zdig.ensure(20 * zc_msgs)) return -1;
-    if (!c->zev) BT_CK(hipEventCreateWithFlags(&c->zev, hipEventDisableTiming));
-    const uint64_t *offs = c->h_zmeta.as<uint64_t>();
-    BT_CK(btsha1_launch_chain(zc_dev, offs, (const uint32_t *)(offs + zc_msgs), 0, 0, zc_msgs,
-                              c->h_zdig.as<uint8_t>(), s, 0, nullptr, nullptr));
-    BT_CK(hipEventRecord(c->zev, s));
-    zc_queued = true;
+  // The split tail: leftovers first (their chain runs beside the columns),
+  // then each column's copy on the idle lane's stream and its hash on the
+  // column stream once that copy is done.  Digest j of the tail (chunk t0 + j)
+  // goes to h_cdig + 20*j; the leftovers' own launch writes theirs after the
+  // tail's (h_cdig + 20*(nchunks - t0) ..) and they are moved into place.
+  const uint64_t ntail = nchunks - sp.t0, rows = sp.c1 - sp.c0, nleft_full = (sp.head ? 1 : 0) + (nfull - sp.c1);
+  auto queue_split = [&](Lane &idle, hipEvent_t last_copied) -> int {
+    if (!sp.parts) return 0;
+    if (!c->cs) {
+      BT_CK(hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+      BT_CK(hipStreamCreateWithFlags(&c->xs, hipStreamNonBlocking));
+      BT_CK(hipEventCreateWithFlags(&c->cdone, hipEventDisableTiming));
+      BT_CK(hipEventCreateWithFlags(&c->xdone, hipEventDisableTiming));
+    }
+    split_queued = true;
+    uint8_t *left = c->h_cleft.as<uint8_t>(), *tdig = c->h_cdig.as<uint8_t>();
+    if (nleft_full || rem) {
+      uint64_t at = 0;
+      if (sp.head) {
+        memcpy(left, h_in + sp.t0 * chunk_len, chunk_len);
+        at = chunk_len;
+      }
+      memcpy(left + at, h_in + sp.c1 * chunk_len, total - sp.c1 * chunk_len);
+      BT_CK(btsha1_launch_chain(left, nullptr, nullptr, chunk_len, chunk_len, nleft_full, tdig + 20 * ntail, c->xs,
+                                rem));
+    }
+    BT_CK(hipEventRecord(c->xdone, c->xs));
+    if (last_copied) BT_CK(hipStreamWaitEvent(idle.s, last_copied, 0));
+    uint8_t *cols = idle.d_in.as<uint8_t>();
+    uint32_t *state = c->d_cstate.as<uint32_t>();
+    const uint64_t w = sp.width;
+    for (uint32_t j = 0; j < sp.parts; ++j) {
+      if (!c->cev[j]) BT_CK(hipEventCreateWithFlags(&c->cev[j], hipEventDisableTiming));
+      const hipError_t ce = hipMemcpy2DAsync(cols + j * rows * w, (size_t)w, h_in + sp.c0 * chunk_len + j * w,
+                                             (size_t)chunk_len, (size_t)w, (size_t)rows, hipMemcpyHostToDevice, idle.s);
+      if (ce != hipSuccess) {
+        set_err("hipMemcpy2DAsync of column %u (%llu x %llu bytes, pitch %llu) from host %p failed: %s", j,
+                (unsigned long long)rows, (unsigned long long)w, (unsigned long long)chunk_len,
+                (const void *)(h_in + sp.c0 * chunk_len + j * w), hipGetErrorString(ce));
+        return -1;
+      }
+      BT_CK(hipEventRecord(c->cev[j], idle.s));
+      BT_CK(hipStreamWaitEvent(c->cs, c->cev[j], 0));
+      const int part = j == 0 ? BTSHA1_COLUMN_FIRST : j + 1 == sp.parts ? BTSHA1_COLUMN_LAST : BTSHA1_COLUMN_MIDDLE;
+      BT_CK(btsha1_launch_column(cols + j * rows * w, rows, (uint32_t)w, (uint32_t)w, part, state, chunk_len,
+                                 tdig + 20 * (sp.c0 - sp.t0), c->cs));
+    }
+    BT_CK(hipEventRecord(c->cdone, c->cs));
     return 0;
   };
-  int64_t n = run_pipeline(c, chunk_len, dma_total, feed, fill, sink, tail);
-  if (n >= 0 && zc_queued) {  // the zero-copy tail's digests follow the copied chunks'
-    const double t0 = now_s();
-    if (hipEventSynchronize(c->zev) != hipSuccess) {
-      set_err("zero-copy tail: %s", hipGetErrorString(hipGetLastError()));
+  auto wait_split = [&]() -> int {
+    if (!split_queued) return 0;
+    BT_CK(hipEventSynchronize(c->cdone));
+    BT_CK(hipEventSynchronize(c->xdone));
+    return 0;
+  };
+  int64_t n = run_pipeline(c, chunk_len, dma_total, feed, fill, sink, tail_ops(queue_split, wait_split));
+  if (n >= 0 && sp.parts) {  // the tail's digests follow the batches'
+    if ((uint64_t)n != sp.t0) {
+      set_err("internal: %lld chunks before the split tail, expected %llu", (long long)n,
+              (unsigned long long)sp.t0);
       n = -1;
     } else {
-      memcpy(h_dig + 20 * (uint64_t)n, c->h_zdig.p, 20 * zc_msgs);
-      n += (int64_t)zc_msgs;
+      const uint8_t *tdig = c->h_cdig.as<uint8_t>();
+      uint8_t *out = h_dig + 20 * sp.t0;
+      memcpy(out + 20 * (sp.c0 - sp.t0), tdig + 20 * (sp.c0 - sp.t0), 20 * rows);
+      const uint8_t *ld = tdig + 20 * ntail;  // leftovers: [head] [c1, nchunks)
+      if (sp.head) {
+        memcpy(out, ld, 20);
+        ld += 20;
+      }
+      memcpy(out + 20 * (sp.c1 - sp.t0), ld, 20 * (nchunks - sp.c1));
+      n = (int64_t)nchunks;
       if (t_stats_valid) {
-        t_stats.chunks = (uint64_t)n;
-        t_stats.zero_copy_chunks = (uint32_t)zc_msgs;
-        t_stats.wait_s += now_s() - t0;
-        t_stats.total_s += now_s() - t0;
+        t_stats.chunks = nchunks;
+        t_stats.column_chunks = (uint32_t)rows;
       }
     }
   }
@@ -1140,19 +1244,20 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
     t_stats.bytes = total;
     page_nodes(h_in, total, 64, t_stats.src_pages, BT_SHA1_STATS_NODES);
   }
-  if (n >= 0 && (feed == Feed::kRegistered || zc_lock)) {  // every batch is done: release the pages (timed)
+  if (n >= 0 && !regs.empty()) {  // every batch is done: release the pages (timed)
     const double t0 = now_s();
     for (void *p : regs)
       if (hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
     const double dt = now_s() - t0;
     if (t_stats_valid) {
-      t_stats.registered_batches = (int32_t)(regs.size() - (zc_lock ? 1 : 0));
+      t_stats.registered_batches = (int32_t)(regs.size() - (sp.lock ? 1 : 0));
       t_stats.register_s = lock_s;
       t_stats.unregister_s = dt;
       t_stats.total_s += lock_s + dt;
     }
     regs.clear();
   }
+  split_queued = false;  // waited for by the pipeline
   return n;
 }
 
@@ -1207,8 +1312,7 @@ int64_t chunks_file_on(int dev, FILE *fp, uint64_t chunk_len, Sink sink) {
     if (r > 0) bytes_in += (uint64_t)r;
     return r;
   };
-  const int64_t n = run_pipeline(c, chunk_len, hint, Feed::kStaged, counted_fill, sink,
-                                 [](hipStream_t, hipEvent_t) { return 0; });
+  const int64_t n = run_pipeline(c, chunk_len, hint, Feed::kStaged, counted_fill, sink, no_tail());
   if (n >= 0 && t_stats_valid) t_stats.bytes = bytes_in;
   if (regular) {
     // Leave the stream where the reference's fread loop leaves it: at EOF,

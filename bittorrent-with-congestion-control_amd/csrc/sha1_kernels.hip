@@ -468,11 +468,23 @@ __device__ __forceinline__ void lat_rounds(State &st, const u32x4 (&q)[20]) {
 // the next block into registers during the current one (60 KiB, so at most
 // two workgroups per CU): it keeps the latency when two workgroups share a
 // CU and their waves share SIMDs (32768 chunks: 6.8 ms vs 11.3 ms).
-template <bool VERIFY, int SLOTS = 2>
+// MID: one COLUMN of each chunk -- len bytes (a 64-byte multiple) at `pitch`
+// from the previous chunk's column -- for the host pipeline's column-split
+// last batch (bt_sha1_api.cpp, chunks_host_on), each chunk's chaining state
+// carried between launches in `state` (word k of chunk i at state[k*n_chunks
+// + i]; SHA1Context.hash, sha.c:446-450):
+//   kLatWhole  (0): whole chunks: IV, blocks, MD padding, digest;
+//   kLatFirst  (1): IV, the column's blocks, state out;
+//   kLatMiddle (2): state in, the column's blocks, state out;
+//   kLatLast   (3): state in, the column's blocks, then the MD padding of a
+//                   msg_len-byte message (sha.c:529-543), digest out.
+constexpr int kLatWhole = 0, kLatFirst = 1, kLatMiddle = 2, kLatLast = 3;
+template <bool VERIFY, int SLOTS = 2, int MID = kLatWhole>
 __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ base, uint64_t n_chunks, uint32_t pitch,
                                                   uint32_t len, uint8_t *__restrict__ digests,
                                                   const uint8_t *__restrict__ expected, uint8_t *__restrict__ ok,
-                                                  uint32_t tail_len) {
+                                                  uint32_t tail_len, uint32_t *__restrict__ state, uint64_t msg_len) {
+  constexpr bool kPad = MID == kLatWhole || MID == kLatLast;  // ends with the MD padding + digest
   __shared__ u32x4 lds[SLOTS][20 * 64];  // SLOTS x 80 words x 64 lanes = SLOTS x 20 KiB
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -490,7 +502,7 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
   const uint32_t nblocks = len >> 6, r = len & 63u;
   // + MD padding block(s).  Both waves execute nb_total + SLOTS - 1 barriers
   // (see "Barrier accounting" above).
-  const uint32_t nb_total = nblocks + (r >= 56u ? 2u : 1u);
+  const uint32_t nb_total = kPad ? nblocks + (r >= 56u ? 2u : 1u) : nblocks;
   uint32_t nbar = 0;
   (void)nbar;
   if (wave == 0) {
@@ -524,28 +536,39 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
         }
       }
     }
-    // Tail bytes + MD padding (sha.c:536-543), as finish() lays them out.
-    uint32_t tail[16];
-    load_tail(tail, rsrc, voff, nblocks, r);
-    const uint32_t wi = r >> 2, mark = 0x80000000u >> ((r & 3) * 8);
+    if constexpr (kPad) {
+      // Tail bytes + MD padding (sha.c:536-543), as finish() lays them out.
+      uint32_t tail[16];
+      load_tail(tail, rsrc, voff, nblocks, r);
+      const uint32_t wi = r >> 2, mark = 0x80000000u >> ((r & 3) * 8);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) tail[j] |= (j == (int)wi) ? mark : 0u;
-    const uint64_t bits = (uint64_t)len * 8ull;
-    if (r >= 56u) {
+      for (int j = 0; j < 16; ++j) tail[j] |= (j == (int)wi) ? mark : 0u;
+      const uint64_t bits = (MID == kLatLast ? msg_len : (uint64_t)len) * 8ull;
+      if (r >= 56u) {
+        produce_block<SLOTS>(tail, lds, slot, lane, nbar);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) tail[j] = 0u;
+      }
+      tail[14] = (uint32_t)(bits >> 32);
+      tail[15] = (uint32_t)bits;
       produce_block<SLOTS>(tail, lds, slot, lane, nbar);
-#pragma unroll
-      for (int j = 0; j < 16; ++j) tail[j] = 0u;
     }
-    tail[14] = (uint32_t)(bits >> 32);
-    tail[15] = (uint32_t)bits;
-    produce_block<SLOTS>(tail, lds, slot, lane, nbar);
 #pragma unroll
     for (int k = 0; k < SLOTS - 1; ++k) BT_LAT_BARRIER(nbar);  // pair with R's last barriers
     BT_LAT_CHECK(nbar, nb_total + SLOTS - 1u);
   } else {
     // ---- R: rounds -----------------------------------------------------------
+    const uint64_t mine = chunk0 + (lane < nvalid ? lane : nvalid - 1u);
     State st;
-    st.init();
+    if constexpr (MID == kLatMiddle || MID == kLatLast) {
+      st.h0 = state[mine];
+      st.h1 = state[n_chunks + mine];
+      st.h2 = state[2 * n_chunks + mine];
+      st.h3 = state[3 * n_chunks + mine];
+      st.h4 = state[4 * n_chunks + mine];
+    } else {
+      st.init();
+    }
     if constexpr (SLOTS == 2) {
       BT_LAT_BARRIER(nbar);  // block 0 is in slot 0
       for (uint32_t b = 0; b < nb_total; ++b) {
@@ -584,7 +607,15 @@ __global__ __launch_bounds__(128) void k_sha1_lat(const uint8_t *__restrict__ ba
       }
     }
     BT_LAT_CHECK(nbar, nb_total + SLOTS - 1u);
-    store_digest<VERIFY>(st, lane, nvalid, chunk0, digests, expected, ok);
+    if constexpr (kPad) {
+      store_digest<VERIFY>(st, lane, nvalid, chunk0, digests, expected, ok);
+    } else if (lane < nvalid) {
+      state[mine] = st.h0;
+      state[n_chunks + mine] = st.h1;
+      state[2 * n_chunks + mine] = st.h2;
+      state[3 * n_chunks + mine] = st.h3;
+      state[4 * n_chunks + mine] = st.h4;
+    }
   }
 }
 
@@ -1174,11 +1205,43 @@ static hipError_t launch_lat_s(const void *d_in, uint64_t n, uint32_t pitch, uin
                                const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s, uint32_t tail_len, uint64_t grid) {
   if (d_ok)
     hipLaunchKernelGGL((k_sha1_lat<true, SLOTS>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_in, n,
-                       pitch, len, d_dig, d_exp, d_ok, tail_len);
+                       pitch, len, d_dig, d_exp, d_ok, tail_len, nullptr, 0ull);
   else
     hipLaunchKernelGGL((k_sha1_lat<false, SLOTS>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_in, n,
-                       pitch, len, d_dig, d_exp, d_ok, tail_len);
+                       pitch, len, d_dig, d_exp, d_ok, tail_len, nullptr, 0ull);
   return hipGetLastError();
+}
+
+template <int SLOTS, int MID>
+static hipError_t launch_column_s(const void *d_col, uint64_t n, uint32_t pitch, uint32_t width, uint32_t *d_state,
+                                  uint64_t msg_len, uint8_t *d_dig, hipStream_t s, uint64_t grid) {
+  hipLaunchKernelGGL((k_sha1_lat<false, SLOTS, MID>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_col, n,
+                     pitch, width, d_dig, nullptr, nullptr, 0u, d_state, msg_len);
+  return hipGetLastError();
+}
+
+template <int MID>
+static hipError_t launch_column_m(const void *d_col, uint64_t n, uint32_t pitch, uint32_t width, uint32_t *d_state,
+                                  uint64_t msg_len, uint8_t *d_dig, hipStream_t s) {
+  const uint64_t grid = (n + 63) / 64;
+  return grid > btsha1_device_cus() ? launch_column_s<3, MID>(d_col, n, pitch, width, d_state, msg_len, d_dig, s, grid)
+                                    : launch_column_s<2, MID>(d_col, n, pitch, width, d_state, msg_len, d_dig, s, grid);
+}
+
+hipError_t btsha1_launch_column(const void *d_col, uint64_t n, uint32_t pitch, uint32_t width, int part,
+                                uint32_t *d_state, uint64_t msg_len, uint8_t *d_dig, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (!d_state || width == 0 || (width & 63u) || pitch < width || (pitch & 15u) || ((uintptr_t)d_col & 15u) ||
+      64 * (uint64_t)pitch >= (1ull << 32))
+    return hipErrorInvalidValue;
+  switch (part) {
+    case BTSHA1_COLUMN_FIRST: return launch_column_m<kLatFirst>(d_col, n, pitch, width, d_state, 0, nullptr, s);
+    case BTSHA1_COLUMN_MIDDLE: return launch_column_m<kLatMiddle>(d_col, n, pitch, width, d_state, 0, nullptr, s);
+    case BTSHA1_COLUMN_LAST:
+      if (!d_dig || ((uintptr_t)d_dig & 3u)) return hipErrorInvalidValue;
+      return launch_column_m<kLatLast>(d_col, n, pitch, width, d_state, msg_len, d_dig, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 static hipError_t launch_lat(const void *d_in, uint64_t n, uint32_t pitch, uint32_t len, uint8_t *d_dig,

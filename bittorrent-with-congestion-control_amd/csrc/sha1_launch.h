@@ -63,6 +63,18 @@ hipError_t btsha1_launch_chain_one(const void *msg, uint64_t len, uint8_t *diges
 hipError_t btsha1_launch_chain(const void *base, const uint64_t *offsets, const uint32_t *lens, uint64_t pitch,
                                uint64_t fixed_len, uint64_t n, uint8_t *digests, hipStream_t s, uint64_t tail_len = 0,
                                const uint8_t *expected = nullptr, uint8_t *ok = nullptr);
+// One column of n equal chunks (k_sha1_lat's column forms): chunk i's column
+// is `width` bytes (a 64-byte multiple) at d_col + i*pitch; d_state holds
+// each chunk's chaining state between columns (5 x n words, word k of chunk i
+// at d_state[k*n + i], device memory).  FIRST starts from the SHA-1 IV,
+// MIDDLE continues, LAST continues and finishes a message of msg_len bytes
+// in all (the column ends the message: msg_len is a 64-byte multiple ending
+// at it), writing digest i (big-endian, 4-byte aligned) to d_dig + 20*i.
+#define BTSHA1_COLUMN_FIRST 0
+#define BTSHA1_COLUMN_MIDDLE 1
+#define BTSHA1_COLUMN_LAST 2
+hipError_t btsha1_launch_column(const void *d_col, uint64_t n, uint32_t pitch, uint32_t width, int part,
+                                uint32_t *d_state, uint64_t msg_len, uint8_t *d_dig, hipStream_t s);
 // Synthetic stream words [first_word, first_word + nbytes/8) into d_buf (16-byte aligned).
 hipError_t btsha1_launch_fill(void *d_buf, uint64_t nbytes, uint64_t first_word, uint64_t seed, hipStream_t s);
 // Digest lookup: d_index[q] = smallest i with table[i] == queries[q], else -1.

@@ -196,11 +196,12 @@ int64_t bt_sha1_chunks_file(void *fp /* FILE* */, uint64_t chunk_len, uint8_t *h
  * first copy and released when the call's last batch is done) and DMA'd in
  * place; the unaligned head
  * and tail bytes of each batch, and pages that cannot be locked, are staged
- * (BT_SHA1_PAGEABLE=stage: stage everything).  The last chunks of such an
- * input (512 by default, at most a quarter; BT_SHA1_ZC_TAIL, 0 = off) are
- * not copied: the kernel reads them straight from the locked host pages while
- * the last copy runs, so the call does not end one chain latency after its
- * last byte crossed PCIe.
+ * (BT_SHA1_PAGEABLE=stage: stage everything).  With pinned or page-locked
+ * input the last ~batch of chunks (at least 256 MiB of them, chunks of at
+ * least 64 KiB) is copied in columns -- 8 strided copies of chunk_len/8
+ * bytes of every chunk (BT_SHA1_COLUMNS: 2..16, 0 = off) -- each hashed into
+ * the chunks' chaining state as soon as it has arrived, so the call ends one
+ * column's hash, not one whole chunk's, after its last byte crossed PCIe.
  * Returns 0, or -1 when this thread has run no pipeline. */
 /* How bt_sha1_chunks_host feeds pageable input of at least 64 MiB to the
  * GPU: page-locked batch by batch and DMA'd in place (REGISTER, the default)
@@ -224,8 +225,8 @@ typedef struct {
   int32_t gpu_numa_node;    /* the GPU's node (-1: unknown)                   */
   int32_t numa_policy;      /* 0 none, 1 lanes, 2 lanes + threads (see above) */
   int32_t registered_batches; /* batches DMA'd from caller pages locked for them */
-  uint32_t zero_copy_chunks;  /* last chunks hashed straight from locked host
-                                 memory, not copied (registered feed)          */
+  uint32_t column_chunks;   /* last chunks copied and hashed column by column
+                               (pinned or page-locked input; see above)      */
   double total_s;           /* the whole call                                 */
   double alloc_s;           /* lane allocation / page-locking in the call     */
   double fill_s;            /* providing the input on the host: staging copies

@@ -95,6 +95,8 @@ int main(int argc, char **argv) {
    * against the staged feed over the same bytes */
   {
     const uint64_t big = 96ull << 20;
+    const char *cmin = getenv("BT_SHA1_COLUMN_MIN_MB");
+    const int split_all = cmin && atol(cmin) == 0;
     uint8_t *pool = malloc(big + 8192);
     for (uint64_t o = 0; o < big + 8192; o += 4 * BT_CHUNK_SIZE) {
       const uint64_t k = big + 8192 - o < 4 * BT_CHUNK_SIZE ? big + 8192 - o : 4 * BT_CHUNK_SIZE;
@@ -103,7 +105,10 @@ int main(int argc, char **argv) {
     }
     for (int t = 0; t < 4; t++) {
       const uint64_t shift = rnd(8192), total = (64ull << 20) + rnd(32u << 20);
-      const uint64_t cl = t == 0 ? BT_CHUNK_SIZE : 4096 * (1 + rnd(200)) + rnd(4096);
+      /* t 0-1: chunks the column-split tail takes (a 512-byte multiple of at
+       * least 64 KiB; split when BT_SHA1_COLUMN_MIN_MB lets a part this small
+       * be), then ragged sizes it leaves alone */
+      const uint64_t cl = t == 0 ? BT_CHUNK_SIZE : t == 1 ? 65536 * (1 + rnd(12)) : 4096 * (1 + rnd(200)) + (rnd(4096) | 1);
       const uint64_t n = (total + cl - 1) / cl;
       uint8_t *a = malloc(20 * n), *b = malloc(20 * n);
       CHECK(bt_sha1_chunks_host(pool + shift, total, cl, a) == (int64_t)n, "registered feed count: %s",
@@ -112,6 +117,8 @@ int main(int argc, char **argv) {
       CHECK(bt_sha1_get_pipeline_stats(&st) == 0 && st.staged == 2 && st.registered_batches == (int32_t)st.batches &&
                 st.chunks == n && st.bytes == total,
             "registered feed stats (feed %d, %d of %u batches locked)", st.staged, st.registered_batches, st.batches);
+      CHECK(!(split_all && t < 2) || st.column_chunks > 0, "no column-split tail (chunk %llu)", (unsigned long long)cl);
+      CHECK(t < 2 || st.column_chunks == 0, "column-split tail of a ragged chunk size %llu", (unsigned long long)cl);
       CHECK(bt_sha1_set_pageable_feed(BT_SHA1_PAGEABLE_STAGE) == BT_SHA1_PAGEABLE_REGISTER, "feed switch");
       CHECK(bt_sha1_chunks_host(pool + shift, total, cl, b) == (int64_t)n, "staged feed count");
       CHECK(bt_sha1_get_pipeline_stats(&st) == 0 && st.staged == 1, "staged feed stats");

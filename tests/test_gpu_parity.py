@@ -594,10 +594,10 @@ def test_pipeline_stats_account_for_each_host_run(bt, oracle, tmp_path):
     wall = time.perf_counter() - t0
     s = bt.pipeline_stats()
     assert (s["chunks"], s["bytes"], s["feed"], s["staged"]) == (151, data.nbytes, "registered", False)
-    # the last min(512, n/4) chunks (the short one included) are hashed zero-copy
-    # from the locked pages; the other 114 (57 MiB, one batch) are copied
-    assert s["zero_copy_chunks"] == 37 and s["batches"] == 1 and s["batch_bytes"] == 114 * CHUNK
-    assert s["registered_batches"] == 1 and s["register_s"] >= 0
+    # two batches of 76 chunks (the input's halves); 76 chunks are too few for
+    # the column-split tail (under 256 MiB)
+    assert s["column_chunks"] == 0 and s["batches"] == 2 and s["batch_bytes"] == 76 * CHUNK
+    assert s["registered_batches"] == 2 and s["register_s"] >= 0
     assert 0 < s["total_s"] <= wall and s["fill_s"] + s["wait_s"] + s["alloc_s"] <= s["total_s"] * 1.001
     assert sum(s["src_pages"]) > 0 and sum(s["copy_pieces"]) == 0   # nothing copied by the staging threads
     bt.host_register(addr, data.nbytes)  # nothing of the call left registered
@@ -605,7 +605,7 @@ def test_pipeline_stats_account_for_each_host_run(bt, oracle, tmp_path):
         assert bt.chunks_host_addr(addr, data.nbytes) == want
         d = bt.pipeline_stats()
         assert (d["chunks"], d["feed"], d["numa_policy"], d["registered_batches"]) == (151, "direct", "none", 0)
-        assert d["zero_copy_chunks"] == 0 and d["batches"] == 2  # the caller's own registration: all copied
+        assert d["column_chunks"] == 0 and d["batches"] == 2
         assert sum(d["copy_pieces"]) == 0 and sum(d["lane_pages"]) == 0
     finally:
         bt.host_unregister(addr)
@@ -637,8 +637,8 @@ def test_pageable_image_registered_batch_by_batch_at_every_alignment(bt, oracle)
         want = b"".join(oracle.hash_chunks(bytes(raw[shift:shift + n]), CHUNK))
         assert bt.chunks_host_addr(addr, n) == want, shift
         s = bt.pipeline_stats()
-        # 35 zero-copy chunks (the short one included, at this odd start) + 106 copied in one batch
-        assert (s["feed"], s["registered_batches"], s["chunks"], s["zero_copy_chunks"]) == ("registered", 1, 141, 35), \
+        # two batches of 71 chunks, each locking its whole pages
+        assert (s["feed"], s["registered_batches"], s["chunks"], s["column_chunks"]) == ("registered", 2, 141, 0), \
             shift
         bt.host_register(addr, n)
         bt.host_unregister(addr)
@@ -668,16 +668,25 @@ def test_registered_feed_falls_back_to_staging_pages_it_cannot_lock(bt, oracle, 
     del ro
 
 
-@pytest.mark.parametrize("env,feed,zc", [({"BT_SHA1_PAGEABLE": "stage"}, "staged", 0),
-                                         ({"BT_SHA1_ZC_TAIL": "0"}, "registered", 0),
-                                         ({"BT_SHA1_ZC_TAIL": "4000"}, "registered", 32),
-                                         ({"BT_SHA1_ZC_TAIL": "7"}, "registered", 7)])
-def test_pageable_feed_knobs(tmp_path, env, feed, zc):
+# 130 chunks + 77 bytes from 5 bytes past a page: the split tail is the last
+# 66 chunks; with the registered feed chunks 65..128 go by columns (chunk 129
+# reaches the input's last, partial page and, like the short one, is hashed
+# from a pinned copy), with the caller's own registration (direct feed) 65..129.
+@pytest.mark.parametrize("env,feed,cols,cols_direct", [
+    ({"BT_SHA1_PAGEABLE": "stage"}, "staged", 0, 65),
+    ({"BT_SHA1_COLUMNS": "0"}, "registered", 0, 0),
+    ({}, "registered", 64, 65),
+    ({"BT_SHA1_COLUMNS": "2"}, "registered", 64, 65),
+    ({"BT_SHA1_COLUMNS": "16"}, "registered", 64, 65),
+    ({"BT_SHA1_COLUMNS": "3"}, "registered", 0, 0),  # no 3-way split of 512 KiB into whole blocks: off
+    ({"BT_SHA1_COLUMN_MIN_MB": "256"}, "registered", 0, 0)])
+def test_pageable_feed_knobs(tmp_path, env, feed, cols, cols_direct):
     """BT_SHA1_PAGEABLE=stage: pageable input of any size is copied into the
-    staging lanes, as before round 6; BT_SHA1_ZC_TAIL sets how many final
-    chunks of the registered feed are hashed straight from the locked host
-    pages (0 = none, capped at a quarter of the input).  Child processes: the
-    knobs are read once.  130 chunks + 77 bytes from an odd start."""
+    staging lanes, as before round 6; BT_SHA1_COLUMNS sets the columns of the
+    column-split tail (0 = off; a count that does not split the chunk into
+    whole 64-byte blocks turns it off) and BT_SHA1_COLUMN_MIN_MB the smallest
+    part it takes (0 here unless given).  Child processes: the knobs are read
+    once.  Exact digests, pageable and then registered by the caller."""
     code = (
         "import sys, numpy as np; sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2]);"
         "import btsha1 as bt, py_oracle as o;"
@@ -686,14 +695,44 @@ def test_pageable_feed_knobs(tmp_path, env, feed, zc):
         "w = b''.join(o.hash_chunks(bytes(d), 524288));"
         "assert bt.chunks_host_addr(d.ctypes.data, d.nbytes) == w;"
         "s = bt.pipeline_stats();"
-        "print('feed', s['feed'], 'zc', s['zero_copy_chunks'], 'chunks', s['chunks'], 'pieces', sum(s['copy_pieces']))")
+        "bt.host_register(d.ctypes.data, d.nbytes);"
+        "assert bt.chunks_host_addr(d.ctypes.data, d.nbytes) == w;"
+        "t = bt.pipeline_stats(); bt.host_unregister(d.ctypes.data);"
+        "print('feed', s['feed'], 'cols', s['column_chunks'], 'chunks', s['chunks'], 'pieces', sum(s['copy_pieces']),"
+        "      'dfeed', t['feed'], 'dcols', t['column_chunks'], 'dchunks', t['chunks'])")
     r = subprocess.run([sys.executable, "-c", code, PKG, os.path.join(REPO, "oracle")], capture_output=True,
-                       text=True, env=dict(os.environ, **env), timeout=120)
+                       text=True, env=dict(os.environ, **{"BT_SHA1_COLUMN_MIN_MB": "0", **env}), timeout=120)
     assert r.returncode == 0, (r.stdout[-1000:], r.stderr[-2000:])
     out = r.stdout.split()
     got = dict(zip(out[::2], out[1::2]))
-    assert (got["feed"], int(got["zc"]), int(got["chunks"])) == (feed, zc, 131), r.stdout
+    assert (got["feed"], int(got["cols"]), int(got["chunks"])) == (feed, cols, 131), r.stdout
+    assert (got["dfeed"], int(got["dcols"]), int(got["dchunks"])) == ("direct", cols_direct, 131), r.stdout
     assert (int(got["pieces"]) > 0) == (feed == "staged")
+
+
+def test_column_split_tail_at_full_size(bt, oracle):
+    """The column-split tail at its default threshold: 1100 chunks + 333 bytes
+    (550 MiB) pageable from an unaligned start, then the same bytes registered
+    by the caller (direct DMA), then a chunk size of 256 KiB: the last ~half
+    goes by columns (275 MiB), digests exact against the oracle, stats say so."""
+    import numpy as np
+    n = 1100 * CHUNK + 333
+    raw = np.empty(n + 4096, dtype=np.uint8)
+    raw.view(np.uint64)[:] = np.arange(raw.size // 8, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    d = raw[100:100 + n]
+    for cl in (CHUNK, CHUNK // 2):
+        want = b"".join(oracle.hash_chunks(d, cl, nthreads=8))
+        nch = (n + cl - 1) // cl
+        assert bt.chunks_host_addr(d.ctypes.data, n, chunk_len=cl) == want, cl
+        s = bt.pipeline_stats()
+        assert (s["feed"], s["chunks"]) == ("registered", nch) and (nch // 2 - 2) <= s["column_chunks"] <= nch // 2, s
+        bt.host_register(d.ctypes.data, n)
+        try:
+            assert bt.chunks_host_addr(d.ctypes.data, n, chunk_len=cl) == want, cl
+            t = bt.pipeline_stats()
+            assert (t["feed"], t["chunks"], t["column_chunks"]) == ("direct", nch, (nch + 1) // 2 - 1), t
+        finally:
+            bt.host_unregister(d.ctypes.data)
 
 
 def test_registered_host_image_direct_dma(bt, oracle):
@@ -839,8 +878,10 @@ def test_host_runtime_under_asan(tmp_path):
     p = tmp_path / "C.tar"
     p.write_bytes(c_tar_bytes())
     ref = [l.split()[1] for l in open(os.path.join(GOLDEN, "ref_C.chunks")).read().splitlines()[2:]]
+    # every registered-feed case with a 512-byte-multiple chunk size takes the
+    # column-split tail (BT_SHA1_COLUMN_MIN_MB=0: however small the part)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0:abort_on_error=0",
-               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", BT_SHA1_COLUMN_MIN_MB="0")
     r = subprocess.run([exe, str(p)] + ref,
                        capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0 and "ok (0 failures)" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

@@ -157,7 +157,10 @@ def _sym(text, prefix):
     return found[0]
 
 
-LAT_SYM = "_ZN6btsha110k_sha1_latILb0ELi2EE"  # k_sha1_lat<false, 2 slots>
+LAT_SYM = "_ZN6btsha110k_sha1_latILb0ELi2ELi0EE"  # k_sha1_lat<false, 2 slots, whole chunks>
+# its column forms (first / middle / last column of the host pipelines'
+# column-split tail): the same round wave
+LAT_COLUMN_SYMS = ["_ZN6btsha110k_sha1_latILb0ELi2ELi%dEE" % m for m in (1, 2, 3)]
 
 
 def _loops(text, sym):
@@ -175,15 +178,17 @@ def _loops(text, sym):
     return out
 
 
-def test_latency_kernel_round_wave_structure(asm):
+@pytest.mark.parametrize("prefix", [LAT_SYM] + LAT_COLUMN_SYMS)
+def test_latency_kernel_round_wave_structure(asm, prefix):
     """k_sha1_lat: the round wave R's loop is one 64-byte block
     per iteration with 5 VALU per round (+ the 5 state adds) = 405, its 80 W+K
     words read as 20 ds_read_b128 from ONE 80-word LDS slot, and exactly one
     s_barrier (the loader wave S pairs it with one barrier per block).  This
-    layout was once lost in a revert and caught only by re-timing."""
+    layout was once lost in a revert and caught only by re-timing.  The
+    column forms (chaining state in / out instead of IV / digest) keep it."""
     import collections
     _, text = asm
-    r_loops = [b for _, b in _loops(text, _sym(text, LAT_SYM)) if "ds_read_b128" in b and "buffer_load" not in b]
+    r_loops = [b for _, b in _loops(text, _sym(text, prefix)) if "ds_read_b128" in b and "buffer_load" not in b]
     assert len(r_loops) == 1, len(r_loops)
     ops = collections.Counter(l.strip().split()[0] for l in r_loops[0].splitlines()
                               if l.strip() and not l.strip().startswith((".", ";")))
@@ -193,13 +198,14 @@ def test_latency_kernel_round_wave_structure(asm):
     assert ops["v_alignbit_b32"] == 160 and ops["v_bitop3_b32"] == 80, ops
 
 
-def test_latency_kernel_loader_ring_keeps_loads_in_flight(asm):
+@pytest.mark.parametrize("prefix", [LAT_SYM] + LAT_COLUMN_SYMS)
+def test_latency_kernel_loader_ring_keeps_loads_in_flight(asm, prefix):
     """S's four-block register ring never waits for the block it just issued:
     the first wait after each group of 16-byte buffer loads leaves >= 4 of them
     outstanding (a vmcnt(0) there would put a memory round trip on every block
     R waits for at the barrier)."""
     _, text = asm
-    waits = _first_wait_after_each_load_group(text, _sym(text, LAT_SYM), load="buffer_load_dwordx4")
+    waits = _first_wait_after_each_load_group(text, _sym(text, prefix), load="buffer_load_dwordx4")
     assert waits, "no buffer load groups found"
     assert min(waits) >= 4, waits
 

@@ -228,12 +228,12 @@ for step in "$@"; do
         -- python3 "$ROOT/tools/stream_bench.py" 4 ;;
     timeline)
       # round 6: kernel + copy trace of 8 GiB pageable chunks_host calls,
-      # zero-copy tail on (default) and off; per-call copy span and tail
-      for zc in 512 0; do
-        mkdir -p "$OUT/tl_$zc"
-        run "tl_$zc" 300 env BT_SHA1_ZC_TAIL=$zc rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
-          -d "$OUT/tl_$zc" -o tl -- python3 "$ROOT/tools/pipeline_timeline.py" 4 8 && \
-        run "tl_${zc}_summary" 120 python3 tools/pipeline_timeline.py --summary "$OUT/tl_$zc" || exit 1
+      # column-split tail on (default 8 columns) and off; per-call copy span and tail
+      for cols in 8 0; do
+        mkdir -p "$OUT/tl_$cols"
+        run "tl_$cols" 300 env BT_SHA1_COLUMNS=$cols rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+          -d "$OUT/tl_$cols" -o tl -- python3 "$ROOT/tools/pipeline_timeline.py" 4 8 && \
+        run "tl_${cols}_summary" 120 python3 tools/pipeline_timeline.py --summary "$OUT/tl_$cols" || exit 1
       done ;;
     latency) run latency 300 python3 tools/latency_bench.py ;;
     numa) run numa 600 python3 tools/numa_probe.py 4 ;;

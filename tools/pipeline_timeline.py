@@ -40,7 +40,7 @@ def run(calls, gib):
         ref = got if ref is None else ref
         print(json.dumps({"call": i, "s": round(t1 - t0, 4), "GiB_per_s": round(img.nbytes / (t1 - t0) / 2**30, 2),
                           "mono_ns": [m0, m1], "same_digests": got == ref,
-                          **{k: st[k] for k in ("feed", "batches", "batch_bytes", "zero_copy_chunks", "wait_s",
+                          **{k: st[k] for k in ("feed", "batches", "batch_bytes", "column_chunks", "wait_s",
                                                 "register_s", "unregister_s")}}), flush=True)
 
 
@@ -58,10 +58,10 @@ def summary(d):
                      for r in rows("*memory_copy_trace.csv")), key=lambda x: x[0])
     # the trace carries no byte counts: the pipeline's batch copies are the H2D ones over 1 ms
     big = [c for c in copies if "HOST_TO_DEVICE" in c[2] and c[1] - c[0] > 1_000_000]
-    # calls: runs of big H2D copies separated by > 50 ms
+    # calls: runs of big H2D copies separated by > 5 ms (within a call they are back to back)
     groups, cur = [], []
     for c in big:
-        if cur and c[0] - cur[-1][1] > 50_000_000:
+        if cur and c[0] - cur[-1][1] > 5_000_000:
             groups.append(cur)
             cur = []
         cur.append(c)
@@ -69,7 +69,8 @@ def summary(d):
         groups.append(cur)
     for gi, g in enumerate(groups):
         c0, c1 = g[0][0], g[-1][1]
-        after = [k for k in kern if c0 <= k[1] and k[0] <= c1 + 100_000_000]
+        nxt = groups[gi + 1][0][0] if gi + 1 < len(groups) else c1 + 100_000_000
+        after = [k for k in kern if c0 <= k[1] and k[0] < nxt]
         tail = [k for k in after if k[1] > c1]
         end = max([c1] + [k[1] for k in tail])
         line = {"call": gi, "copies": len(g), "copy_span_ms": round((c1 - c0) / 1e6, 3),

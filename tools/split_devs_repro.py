@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""tools/zc_devs_repro.py -- a pageable image split over repeated worker ids
-(bt_sha1_chunks_host_devices, devs=[0]*W) through the registered feed with
-its zero-copy tail: digests against one worker's, each image start offset.
-usage: zc_devs_repro.py [GiB] [workers]"""
+"""tools/split_devs_repro.py -- a pageable image split over repeated worker
+ids (bt_sha1_chunks_host_devices, devs=[0]*W) through the registered feed
+with its column-split tail: digests against one worker's, each image start
+offset.
+usage: split_devs_repro.py [GiB] [workers]"""
 import os
 import sys
 
@@ -18,14 +19,14 @@ w = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 n = int(gib * 2048)
 raw = np.empty(n * 524288 + 8192, dtype=np.uint8)
 raw.view(np.uint64)[:] = np.arange(raw.size // 8, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
-print("base mod 4096:", raw.ctypes.data % 4096, "ZC", os.environ.get("BT_SHA1_ZC_TAIL"), flush=True)
+print("base mod 4096:", raw.ctypes.data % 4096, "columns", os.environ.get("BT_SHA1_COLUMNS"), flush=True)
 for shift in (0, 16, (-raw.ctypes.data) % 4096):
     addr, nbytes = raw.ctypes.data + shift, n * 524288
     one = bt.chunks_host_addr(addr, nbytes)
     st = bt.pipeline_stats()
     try:
         many = bt.chunks_host_addr(addr, nbytes, devs=[0] * w)
-        print("shift", shift, "single zc", st["zero_copy_chunks"], "devs ok" if many == one else "devs MISMATCH",
+        print("shift", shift, "single column chunks", st["column_chunks"], "devs ok" if many == one else "devs MISMATCH",
               flush=True)
     except bt.BtSha1Error as e:
         print("shift", shift, "devs ERROR", e, flush=True)

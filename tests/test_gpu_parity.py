@@ -717,7 +717,7 @@ def test_column_split_tail_at_full_size(bt, oracle):
     goes by columns (275 MiB), digests exact against the oracle, stats say so."""
     import numpy as np
     n = 1100 * CHUNK + 333
-    raw = np.empty(n + 4096, dtype=np.uint8)
+    raw = np.empty(n + 4096 - n % 8, dtype=np.uint8)
     raw.view(np.uint64)[:] = np.arange(raw.size // 8, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
     d = raw[100:100 + n]
     for cl in (CHUNK, CHUNK // 2):

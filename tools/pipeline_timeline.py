@@ -8,8 +8,8 @@ with bt_sha1_chunks_host `calls` times; each call's wall interval is printed
 (perf_counter and, for matching against the trace, CLOCK_MONOTONIC ns, the
 clock rocprofv3 stamps with) beside the library's pipeline stats.  With
 `--summary DIR` instead, reads the trace CSVs rocprofv3 wrote under DIR and
-prints, per call: copy start/end, the kernels after the last copy, and the
-gaps between them.
+prints, per call: the copies (b = a lane batch, c = a column of the split
+tail), the gaps between them, and the kernels still running after the last.
 usage: pipeline_timeline.py [calls] [GiB]  |  pipeline_timeline.py --summary DIR
 """
 import csv
@@ -56,12 +56,15 @@ def summary(d):
                    for r in rows("*kernel_trace.csv")), key=lambda x: x[0])
     copies = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Direction", ""))
                      for r in rows("*memory_copy_trace.csv")), key=lambda x: x[0])
-    # the trace carries no byte counts: the pipeline's batch copies are the H2D ones over 1 ms
-    big = [c for c in copies if "HOST_TO_DEVICE" in c[2] and c[1] - c[0] > 1_000_000]
-    # calls: runs of big H2D copies separated by > 5 ms (within a call they are back to back)
+    # the trace carries no byte counts: the pipeline's batch copies are the H2D
+    # ones over 1 ms; the column-split tail's strided copies out of locked host
+    # pages are traced as DEVICE_TO_DEVICE (the runtime sees a device-mapped
+    # source) -- "column" in copy_kinds
+    big = [c for c in copies if ("HOST_TO_DEVICE" in c[2] or "DEVICE_TO_DEVICE" in c[2]) and c[1] - c[0] > 1_000_000]
+    # calls: runs of copies separated by > 0.5 ms (within a call they are back to back)
     groups, cur = [], []
     for c in big:
-        if cur and c[0] - cur[-1][1] > 5_000_000:
+        if cur and c[0] - cur[-1][1] > 500_000:
             groups.append(cur)
             cur = []
         cur.append(c)
@@ -76,6 +79,7 @@ def summary(d):
         line = {"call": gi, "copies": len(g), "copy_span_ms": round((c1 - c0) / 1e6, 3),
                 "copy_gaps_ms": [round((g[i + 1][0] - g[i][1]) / 1e6, 3) for i in range(len(g) - 1)],
                 "copy_ms": [round((c[1] - c[0]) / 1e6, 3) for c in g],
+                "copy_kinds": "".join("c" if "DEVICE_TO_DEVICE" in c[2] else "b" for c in g),
                 "end_after_last_copy_ms": round((end - c1) / 1e6, 3),
                 "tail_kernels": [{"name": k[2], "start_ms": round((k[0] - c1) / 1e6, 3),
                                   "dur_ms": round((k[1] - k[0]) / 1e6, 3)} for k in tail],

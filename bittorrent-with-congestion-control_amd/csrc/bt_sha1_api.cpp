@@ -969,6 +969,10 @@ bool register_pageable() { return pageable_feed() == BT_SHA1_PAGEABLE_REGISTER; 
 // device's shared context.
 int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t chunk_len, uint8_t *h_dig,
                        DevCtx *own = nullptr) {
+  if (chunk_len == 0 || chunk_len >= (1ull << 32)) {  // before any chunk arithmetic
+    set_err("chunk_len must be in [1, 4 GiB)");
+    return -1;
+  }
   KeepDevice keep_dev;
   DevCtx *c = own ? own : ctx_for(dev);
   if (!c) return -1;

@@ -278,6 +278,18 @@ def test_verify_stream_rejects_bad_options_before_any_gpu_call(tmp_path, args, m
     assert r.returncode == 255 and msg in r.stderr, (r.returncode, r.stderr)
 
 
+def test_chunk_len_checked_before_any_chunk_arithmetic():
+    """bt_sha1_chunks_host with chunk_len 0 or >= 4 GiB (the kernels' 32-bit
+    lengths) is -1 with a message, before any device call or division by the
+    chunk length."""
+    bt = load_btsha1()
+    buf = (ctypes.c_uint8 * 4096)()
+    out = (ctypes.c_uint8 * 20)()
+    for cl in (0, 1 << 32):
+        assert bt.lib.bt_sha1_chunks_host(buf, 4096, cl, out) == -1, cl
+        assert "chunk_len must be in [1, 4 GiB)" in bt.last_error(), cl
+
+
 def test_pageable_feed_switch_needs_no_device():
     """bt_sha1_set_pageable_feed: REGISTER (0, the default) / STAGE (1) swap
     and report the previous setting; anything else is -1 with a message; no

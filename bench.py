@@ -548,16 +548,18 @@ def cpu_baseline(host_addr, n_chunks, gpu_digests, min_s=1.0, reps=3):
                 "sample_chunks": n, "passes": passes, "digests_match_gpu": ok}
 
     n1 = max(min(256, n_chunks), n_chunks // 4)
-    rows, kind = {}, None
+    rows, kind, run_flags = {}, None, {}
     for opt, flags in (("O2", "-O2"), ("O0", "-g -O0 (reference Makefile:3)")):
         k, fn = pick(opt)
         if fn is None:
             continue
         kind = kind or k
+        run_flags[opt] = flags
         counts = {1, cores} | ({affinity} if opt == "O2" else set())
         for nt in sorted(counts):
             r = run(fn, nt, n1 if nt == 1 else n_chunks)
-            rows[f"{opt}_{nt}t"] = {**r, "threads": nt, "flags": flags, "kind": k}
+            # a run's flags are its key's prefix (run_flags); its kind only when it differs
+            rows[f"{opt}_{nt}t"] = {**r, "threads": nt, **({"kind": k} if k != kind else {})}
     # value: the best sustained -O2 rate over the multi-thread runs (`cores`
     # threads, one per CPU of the affinity mask); both are bounded by the
     # quota, and with exactly `cores` threads the process's other threads
@@ -570,10 +572,10 @@ def cpu_baseline(host_addr, n_chunks, gpu_digests, min_s=1.0, reps=3):
         "sample": f"{n_chunks} x 512 KiB of the bench's chunks ({n1} on 1 thread), shahash per chunk (chunk.c:21); "
                   f"rate = median of {reps} runs of >= {min_s:g} s; value = best -O2 multi-thread run; cores = "
                   f"min(affinity {affinity}, ceil(quota {quota}))",
-        "flags": head["flags"], "digests_match_gpu": all(r["digests_match_gpu"] for r in rows.values()),
+        "flags": run_flags.get("O2"), "digests_match_gpu": all(r["digests_match_gpu"] for r in rows.values()),
         "per_core_GiB_per_s_O2": per_core,
         "quota_bound_GiB_per_s": round(per_core * quota, 3) if per_core and quota else None,
-        "runs": rows, "machine_cpus": machine, "affinity_cpus": affinity,
+        "runs": rows, "run_flags": run_flags, "machine_cpus": machine, "affinity_cpus": affinity,
         "cgroup_cpu_quota": quota, "host_cpu": cpu_model(),
     }
 

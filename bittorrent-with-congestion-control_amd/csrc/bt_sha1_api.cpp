@@ -622,6 +622,21 @@ void parallel_copy(uint8_t *dst, const uint8_t *src, uint64_t n) {
   parallel_pieces(n, [&](uint64_t off, uint64_t len, int) { memcpy(dst + off, src + off, len); }, true);
 }
 
+// Gather one column of `rows` strided rows into a dense buffer with the copy
+// threads: dst[r*width ..] = src[r*pitch ..] (width bytes per row).
+void parallel_gather(uint8_t *dst, const uint8_t *src, uint64_t rows, uint64_t width, uint64_t pitch) {
+  parallel_pieces(
+      rows * width,
+      [&](uint64_t off, uint64_t len, int) {
+        for (uint64_t o = off, end = off + len; o < end;) {
+          const uint64_t r = o / width, in = o % width, k = std::min<uint64_t>(width - in, end - o);
+          memcpy(dst + o, src + r * pitch + in, k);
+          o += k;
+        }
+      },
+      true);
+}
+
 // pread `want` bytes at file offset `pos` into dst with several threads.
 // Returns the length of the contiguous prefix read (short only at EOF), or -1.
 int64_t parallel_pread(int fd, uint8_t *dst, uint64_t want, uint64_t pos) {
@@ -1023,7 +1038,7 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
     void *lock = nullptr;             // registered feed: the columns' locked pages
   } sp;
   const double t_lock0 = now_s();
-  if (feed != Feed::kStaged) {
+  {
     uint32_t parts = columns();
     while (parts >= 2 && chunk_len % (64ull * parts)) parts /= 2;
     const uint64_t per = batch_bytes_for(chunk_len, total, false) / chunk_len;
@@ -1116,11 +1131,20 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   }
   // The columns land in the lane that is idle once the last batch is queued
   // (its previous batch's hash precedes them on its stream): sized for them
-  // up front, never grown while a batch may still read it.
+  // up front, never grown while a batch may still read it -- its device
+  // buffer, and for the staged feed its staging (on the GPU's node, as the
+  // pipeline places it), where the copy threads gather the columns.
   if (sp.parts) {
-    const int k_last = dma_total ? (int)((dma_total + batch - 1) / batch) : 0;
-    if (c->lane[k_last & 1].d_in.ensure(std::max<uint64_t>((sp.c1 - sp.c0) * chunk_len, dma_total ? batch : 0)))
-      return -1;
+    const bool staged = feed == Feed::kStaged;
+    const uint64_t lane_batch = batch_bytes_for(chunk_len, dma_total, staged);
+    const int k_last = dma_total ? (int)((dma_total + lane_batch - 1) / lane_batch) : 0;
+    const uint64_t need = std::max<uint64_t>((sp.c1 - sp.c0) * chunk_len, dma_total ? lane_batch : 0);
+    Lane &idle = c->lane[k_last & 1];
+    if (idle.d_in.ensure(need)) return -1;
+    if (staged) {
+      if (c->numa_node == -2) c->numa_node = gpu_numa_node(c->dev);
+      if (idle.h_in.ensure(need, placement_for(c->numa_node).node)) return -1;
+    }
   }
   uint64_t b1 = 0, p0 = 0, p1 = 0;
   bool locked = false;
@@ -1171,6 +1195,7 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   // goes to h_cdig + 20*j; the leftovers' own launch writes theirs after the
   // tail's (h_cdig + 20*(nchunks - t0) ..) and they are moved into place.
   const uint64_t ntail = nchunks - sp.t0, rows = sp.c1 - sp.c0, nleft_full = (sp.head ? 1 : 0) + (nfull - sp.c1);
+  double t_gather = 0;  // staged feed: host time gathering the columns
   auto queue_split = [&](Lane &idle, hipEvent_t last_copied) -> int {
     if (!sp.parts) return 0;
     if (!c->cs) {
@@ -1193,17 +1218,32 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
     }
     BT_CK(hipEventRecord(c->xdone, c->xs));
     if (last_copied) BT_CK(hipStreamWaitEvent(idle.s, last_copied, 0));
-    uint8_t *cols = idle.d_in.as<uint8_t>();
+    // Staged feed: the copy threads gather each column into the idle lane's
+    // staging (free once its previous batch is done) while the previous
+    // column crosses PCIe; pinned / locked input: one strided copy per column.
+    const bool staged = feed == Feed::kStaged;
+    if (staged && idle.busy) BT_CK(hipEventSynchronize(idle.ev));
+    uint8_t *cols = idle.d_in.as<uint8_t>(), *stage = staged ? idle.h_in.as<uint8_t>() : nullptr;
     uint32_t *state = c->d_cstate.as<uint32_t>();
     const uint64_t w = sp.width;
     for (uint32_t j = 0; j < sp.parts; ++j) {
       if (!c->cev[j]) BT_CK(hipEventCreateWithFlags(&c->cev[j], hipEventDisableTiming));
-      const hipError_t ce = hipMemcpy2DAsync(cols + j * rows * w, (size_t)w, h_in + sp.c0 * chunk_len + j * w,
-                                             (size_t)chunk_len, (size_t)w, (size_t)rows, hipMemcpyHostToDevice, idle.s);
+      const uint8_t *src = h_in + sp.c0 * chunk_len + j * w;
+      hipError_t ce;
+      if (staged) {
+        const double g0 = now_s();
+        parallel_gather(stage + j * rows * w, src, rows, w, chunk_len);
+        t_gather += now_s() - g0;
+        ce = hipMemcpyAsync(cols + j * rows * w, stage + j * rows * w, (size_t)(rows * w), hipMemcpyHostToDevice,
+                            idle.s);
+      } else {
+        ce = hipMemcpy2DAsync(cols + j * rows * w, (size_t)w, src, (size_t)chunk_len, (size_t)w, (size_t)rows,
+                              hipMemcpyHostToDevice, idle.s);
+      }
       if (ce != hipSuccess) {
-        set_err("hipMemcpy2DAsync of column %u (%llu x %llu bytes, pitch %llu) from host %p failed: %s", j,
-                (unsigned long long)rows, (unsigned long long)w, (unsigned long long)chunk_len,
-                (const void *)(h_in + sp.c0 * chunk_len + j * w), hipGetErrorString(ce));
+        set_err("copy of column %u (%llu x %llu bytes, pitch %llu) from host %p failed: %s", j,
+                (unsigned long long)rows, (unsigned long long)w, (unsigned long long)chunk_len, (const void *)src,
+                hipGetErrorString(ce));
         return -1;
       }
       BT_CK(hipEventRecord(c->cev[j], idle.s));
@@ -1241,6 +1281,7 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
       if (t_stats_valid) {
         t_stats.chunks = nchunks;
         t_stats.column_chunks = (uint32_t)rows;
+        t_stats.fill_s += t_gather;
       }
     }
   }

@@ -673,7 +673,7 @@ def test_registered_feed_falls_back_to_staging_pages_it_cannot_lock(bt, oracle, 
 # reaches the input's last, partial page and, like the short one, is hashed
 # from a pinned copy), with the caller's own registration (direct feed) 65..129.
 @pytest.mark.parametrize("env,feed,cols,cols_direct", [
-    ({"BT_SHA1_PAGEABLE": "stage"}, "staged", 0, 65),
+    ({"BT_SHA1_PAGEABLE": "stage"}, "staged", 65, 65),  # staged: no page constraint, only the short chunk left over
     ({"BT_SHA1_COLUMNS": "0"}, "registered", 0, 0),
     ({}, "registered", 64, 65),
     ({"BT_SHA1_COLUMNS": "2"}, "registered", 64, 65),
@@ -682,7 +682,8 @@ def test_registered_feed_falls_back_to_staging_pages_it_cannot_lock(bt, oracle, 
     ({"BT_SHA1_COLUMN_MIN_MB": "256"}, "registered", 0, 0)])
 def test_pageable_feed_knobs(tmp_path, env, feed, cols, cols_direct):
     """BT_SHA1_PAGEABLE=stage: pageable input of any size is copied into the
-    staging lanes, as before round 6; BT_SHA1_COLUMNS sets the columns of the
+    staging lanes, as before round 6 (its split tail's columns gathered there
+    by the copy threads); BT_SHA1_COLUMNS sets the columns of the
     column-split tail (0 = off; a count that does not split the chunk into
     whole 64-byte blocks turns it off) and BT_SHA1_COLUMN_MIN_MB the smallest
     part it takes (0 here unless given).  Child processes: the knobs are read
@@ -712,9 +713,10 @@ def test_pageable_feed_knobs(tmp_path, env, feed, cols, cols_direct):
 
 def test_column_split_tail_at_full_size(bt, oracle):
     """The column-split tail at its default threshold: 1100 chunks + 333 bytes
-    (550 MiB) pageable from an unaligned start, then the same bytes registered
-    by the caller (direct DMA), then a chunk size of 256 KiB: the last ~half
-    goes by columns (275 MiB), digests exact against the oracle, stats say so."""
+    (550 MiB) pageable from an unaligned start, the same bytes registered by
+    the caller (direct DMA), and staged; then a chunk size of 256 KiB: the
+    last ~half goes by columns (275 MiB), digests exact against the oracle,
+    stats say so."""
     import numpy as np
     n = 1100 * CHUNK + 333
     raw = np.empty(n + 4096 - n % 8, dtype=np.uint8)
@@ -733,6 +735,14 @@ def test_column_split_tail_at_full_size(bt, oracle):
             assert (t["feed"], t["chunks"], t["column_chunks"]) == ("direct", nch, (nch + 1) // 2 - 1), t
         finally:
             bt.host_unregister(d.ctypes.data)
+        prev = bt.set_pageable_feed("stage")  # the copy threads gather the columns into the staging lane
+        try:
+            assert bt.chunks_host_addr(d.ctypes.data, n, chunk_len=cl) == want, cl
+            u = bt.pipeline_stats()
+            assert (u["feed"], u["chunks"], u["column_chunks"]) == ("staged", nch, (nch + 1) // 2 - 1), u
+            assert u["fill_s"] > 0 and sum(u["copy_pieces"]) > 0
+        finally:
+            bt.set_pageable_feed(prev)
 
 
 def test_registered_host_image_direct_dma(bt, oracle):

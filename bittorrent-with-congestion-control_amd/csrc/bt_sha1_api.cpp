@@ -1041,7 +1041,12 @@ int64_t chunks_host_on(int dev, const uint8_t *h_in, uint64_t total, uint64_t ch
   {
     uint32_t parts = columns();
     while (parts >= 2 && chunk_len % (64ull * parts)) parts /= 2;
-    const uint64_t per = batch_bytes_for(chunk_len, total, false) / chunk_len;
+    // about one batch of this feed, never more than a kept lane holds
+    // (1 GiB: the idle lane carries the columns, and a staged lane is never
+    // shrunk after the call)
+    const uint64_t per = std::min<uint64_t>(batch_bytes_for(chunk_len, total, feed == Feed::kStaged),
+                                            batch_bytes_for(chunk_len, UINT64_MAX, true)) /
+                         chunk_len;
     const uint64_t t0 = nchunks - std::min<uint64_t>(nchunks, per);
     uint64_t c0 = t0, c1 = nfull;
     const uintptr_t base = (uintptr_t)h_in;

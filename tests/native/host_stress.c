@@ -11,6 +11,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "bt_sha1.h"
 #include "chunk.h"
@@ -186,5 +187,12 @@ int main(int argc, char **argv) {
   bt_sha1_verifier_destroy(v);
   free(img);
   printf("%s (%d failures)\n", fails ? "FAILED" : "ok", fails);
-  return fails != 0;
+  /* Leave without running the HIP runtime's own static teardown: under the
+   * host ASan runtime it can free queue memory after ASan has marked the HSA
+   * runtime unloaded (an ASan CHECK inside libhsa-runtime's finalizers, seen
+   * once in this test's history), which is not what this stress test checks
+   * and would also lose the buffered verdict above. */
+  fflush(stdout);
+  fflush(stderr);
+  _exit(fails != 0);
 }

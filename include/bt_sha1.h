@@ -196,12 +196,14 @@ int64_t bt_sha1_chunks_file(void *fp /* FILE* */, uint64_t chunk_len, uint8_t *h
  * first copy and released when the call's last batch is done) and DMA'd in
  * place; the unaligned head
  * and tail bytes of each batch, and pages that cannot be locked, are staged
- * (BT_SHA1_PAGEABLE=stage: stage everything).  With pinned or page-locked
- * input the last ~batch of chunks (at least 256 MiB of them, chunks of at
- * least 64 KiB) is copied in columns -- 8 strided copies of chunk_len/8
- * bytes of every chunk (BT_SHA1_COLUMNS: 2..16, 0 = off) -- each hashed into
- * the chunks' chaining state as soon as it has arrived, so the call ends one
- * column's hash, not one whole chunk's, after its last byte crossed PCIe.
+ * (BT_SHA1_PAGEABLE=stage: stage everything).  The last ~batch of chunks of
+ * a bt_sha1_chunks_host input (at least 256 MiB of them, chunks of at least
+ * 64 KiB; BT_SHA1_COLUMN_MIN_MB) is copied in columns -- 8 strided copies of
+ * chunk_len/8 bytes of every chunk (BT_SHA1_COLUMNS: 2..16, 0 = off), for the
+ * staged feed gathered into the staging lane by the copy threads -- each
+ * hashed into the chunks' chaining state as soon as it has arrived, so the
+ * call ends one column's hash, not one whole chunk's, after its last byte
+ * crossed PCIe.
  * Returns 0, or -1 when this thread has run no pipeline. */
 /* How bt_sha1_chunks_host feeds pageable input of at least 64 MiB to the
  * GPU: page-locked batch by batch and DMA'd in place (REGISTER, the default)
@@ -226,7 +228,7 @@ typedef struct {
   int32_t numa_policy;      /* 0 none, 1 lanes, 2 lanes + threads (see above) */
   int32_t registered_batches; /* batches DMA'd from caller pages locked for them */
   uint32_t column_chunks;   /* last chunks copied and hashed column by column
-                               (pinned or page-locked input; see above)      */
+                               (bt_sha1_chunks_host; see above)              */
   double total_s;           /* the whole call                                 */
   double alloc_s;           /* lane allocation / page-locking in the call     */
   double fill_s;            /* providing the input on the host: staging copies

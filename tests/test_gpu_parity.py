@@ -714,15 +714,17 @@ def test_pageable_feed_knobs(tmp_path, env, feed, cols, cols_direct):
 def test_column_split_tail_at_full_size(bt, oracle):
     """The column-split tail at its default threshold: 1100 chunks + 333 bytes
     (550 MiB) pageable from an unaligned start, the same bytes registered by
-    the caller (direct DMA), and staged; then a chunk size of 256 KiB: the
-    last ~half goes by columns (275 MiB), digests exact against the oracle,
-    stats say so."""
+    the caller (direct DMA), and staged; at chunk sizes of 512, 256, 192 and
+    64 KiB: the last ~half goes by columns (275 MiB), digests exact against
+    the oracle, stats say so."""
     import numpy as np
     n = 1100 * CHUNK + 333
     raw = np.empty(n + 4096 - n % 8, dtype=np.uint8)
     raw.view(np.uint64)[:] = np.arange(raw.size // 8, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
     d = raw[100:100 + n]
-    for cl in (CHUNK, CHUNK // 2):
+    # 512 / 256 KiB, the smallest chunk the split takes (64 KiB: 4 KiB columns,
+    # 4400 rows), and one that is no power of two (192 KiB: 24 KiB columns)
+    for cl in (CHUNK, CHUNK // 2, 65536, 196608):
         want = b"".join(oracle.hash_chunks(d, cl, nthreads=8))
         nch = (n + cl - 1) // cl
         assert bt.chunks_host_addr(d.ctypes.data, n, chunk_len=cl) == want, cl

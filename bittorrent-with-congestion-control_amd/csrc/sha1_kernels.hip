@@ -1212,34 +1212,41 @@ static hipError_t launch_lat_s(const void *d_in, uint64_t n, uint32_t pitch, uin
   return hipGetLastError();
 }
 
-template <int SLOTS, int MID>
+template <int SLOTS, int MID, bool VERIFY = false>
 static hipError_t launch_column_s(const void *d_col, uint64_t n, uint32_t pitch, uint32_t width, uint32_t *d_state,
-                                  uint64_t msg_len, uint8_t *d_dig, hipStream_t s, uint64_t grid) {
-  hipLaunchKernelGGL((k_sha1_lat<false, SLOTS, MID>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_col, n,
-                     pitch, width, d_dig, nullptr, nullptr, 0u, d_state, msg_len);
+                                  uint64_t msg_len, uint8_t *d_dig, const uint8_t *d_exp, uint8_t *d_ok, hipStream_t s,
+                                  uint64_t grid) {
+  hipLaunchKernelGGL((k_sha1_lat<VERIFY, SLOTS, MID>), dim3((uint32_t)grid), dim3(128), 0, s, (const uint8_t *)d_col, n,
+                     pitch, width, d_dig, d_exp, d_ok, 0u, d_state, msg_len);
   return hipGetLastError();
 }
 
-template <int MID>
+template <int MID, bool VERIFY = false>
 static hipError_t launch_column_m(const void *d_col, uint64_t n, uint32_t pitch, uint32_t width, uint32_t *d_state,
-                                  uint64_t msg_len, uint8_t *d_dig, hipStream_t s) {
+                                  uint64_t msg_len, uint8_t *d_dig, const uint8_t *d_exp, uint8_t *d_ok,
+                                  hipStream_t s) {
   const uint64_t grid = (n + 63) / 64;
-  return grid > btsha1_device_cus() ? launch_column_s<3, MID>(d_col, n, pitch, width, d_state, msg_len, d_dig, s, grid)
-                                    : launch_column_s<2, MID>(d_col, n, pitch, width, d_state, msg_len, d_dig, s, grid);
+  return grid > btsha1_device_cus()
+             ? launch_column_s<3, MID, VERIFY>(d_col, n, pitch, width, d_state, msg_len, d_dig, d_exp, d_ok, s, grid)
+             : launch_column_s<2, MID, VERIFY>(d_col, n, pitch, width, d_state, msg_len, d_dig, d_exp, d_ok, s, grid);
 }
 
 hipError_t btsha1_launch_column(const void *d_col, uint64_t n, uint32_t pitch, uint32_t width, int part,
-                                uint32_t *d_state, uint64_t msg_len, uint8_t *d_dig, hipStream_t s) {
+                                uint32_t *d_state, uint64_t msg_len, uint8_t *d_dig, hipStream_t s,
+                                const uint8_t *d_exp, uint8_t *d_ok) {
   if (n == 0) return hipSuccess;
   if (!d_state || width == 0 || (width & 63u) || pitch < width || (pitch & 15u) || ((uintptr_t)d_col & 15u) ||
-      64 * (uint64_t)pitch >= (1ull << 32))
+      64 * (uint64_t)pitch >= (1ull << 32) || (d_ok && (!d_exp || part != BTSHA1_COLUMN_LAST)))
     return hipErrorInvalidValue;
   switch (part) {
-    case BTSHA1_COLUMN_FIRST: return launch_column_m<kLatFirst>(d_col, n, pitch, width, d_state, 0, nullptr, s);
-    case BTSHA1_COLUMN_MIDDLE: return launch_column_m<kLatMiddle>(d_col, n, pitch, width, d_state, 0, nullptr, s);
+    case BTSHA1_COLUMN_FIRST:
+      return launch_column_m<kLatFirst>(d_col, n, pitch, width, d_state, 0, nullptr, nullptr, nullptr, s);
+    case BTSHA1_COLUMN_MIDDLE:
+      return launch_column_m<kLatMiddle>(d_col, n, pitch, width, d_state, 0, nullptr, nullptr, nullptr, s);
     case BTSHA1_COLUMN_LAST:
-      if (!d_dig || ((uintptr_t)d_dig & 3u)) return hipErrorInvalidValue;
-      return launch_column_m<kLatLast>(d_col, n, pitch, width, d_state, msg_len, d_dig, s);
+      if ((!d_dig && !d_ok) || ((uintptr_t)d_dig & 3u)) return hipErrorInvalidValue;
+      return d_ok ? launch_column_m<kLatLast, true>(d_col, n, pitch, width, d_state, msg_len, d_dig, d_exp, d_ok, s)
+                  : launch_column_m<kLatLast>(d_col, n, pitch, width, d_state, msg_len, d_dig, nullptr, nullptr, s);
     default: return hipErrorInvalidValue;
   }
 }

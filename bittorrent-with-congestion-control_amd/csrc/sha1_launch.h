@@ -69,12 +69,15 @@ hipError_t btsha1_launch_chain(const void *base, const uint64_t *offsets, const 
 // at d_state[k*n + i], device memory).  FIRST starts from the SHA-1 IV,
 // MIDDLE continues, LAST continues and finishes a message of msg_len bytes
 // in all (the column ends the message: msg_len is a 64-byte multiple ending
-// at it), writing digest i (big-endian, 4-byte aligned) to d_dig + 20*i.
+// at it), writing digest i (big-endian, 4-byte aligned) to d_dig + 20*i, and
+// with d_ok (LAST only) also ok[i] = digest i == d_exp[20*i ..] (util.c:313;
+// d_dig may then be NULL).
 #define BTSHA1_COLUMN_FIRST 0
 #define BTSHA1_COLUMN_MIDDLE 1
 #define BTSHA1_COLUMN_LAST 2
 hipError_t btsha1_launch_column(const void *d_col, uint64_t n, uint32_t pitch, uint32_t width, int part,
-                                uint32_t *d_state, uint64_t msg_len, uint8_t *d_dig, hipStream_t s);
+                                uint32_t *d_state, uint64_t msg_len, uint8_t *d_dig, hipStream_t s,
+                                const uint8_t *d_exp = nullptr, uint8_t *d_ok = nullptr);
 // Synthetic stream words [first_word, first_word + nbytes/8) into d_buf (16-byte aligned).
 hipError_t btsha1_launch_fill(void *d_buf, uint64_t nbytes, uint64_t first_word, uint64_t seed, hipStream_t s);
 // Digest lookup: d_index[q] = smallest i with table[i] == queries[q], else -1.

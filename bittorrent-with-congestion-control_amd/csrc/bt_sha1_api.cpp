@@ -2101,7 +2101,11 @@ int v_launch(bt_sha1_verifier *v, uint32_t idx) {
     return 0;
   }
   if (const uint32_t parts = v_columns(v->chunk_len, b.reserved)) {
-    if (v_launch_columns(v, b, parts)) return -1;
+    if (v_launch_columns(v, b, parts)) {  // leave nothing of the batch in flight behind the error
+      if (b.s) (void)hipStreamSynchronize(b.s);
+      if (b.hs) (void)hipStreamSynchronize(b.hs);
+      return -1;
+    }
     b.inflight = true;
     v->order.push_back(idx);
     return 0;
